@@ -1,0 +1,301 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: device-resident RLNC encode+decode GiB/s, k=32 × 1 MiB, 1/2/4/8 MI355X.
+
+One step = for each of --objects independent objects resident in HBM (16 × 32 MiB = 512 MiB of source per
+GPU, more than the 256 MiB Infinity Cache so source reads come from HBM):
+  * encode: 32 source pieces × 1 MiB → 64 full coded pieces (BASELINE configs[1]); one kernel launch for all
+    objects (librlnc_hip rlnc_encode_batch);
+  * decode: feed the first 32 coded pieces of every object to a fresh Decoder (configs[2]): exact
+    diagonal-pivot elimination of the coefficient block per piece (host), then T × data on the device,
+    then the boundary-marker scan (rlnc_decode_batch).
+`value` = GiB/s in the reference's own byte counters (SURVEY.md §6 / BASELINE.md): per object
+64 × (k·L + k + L) for the 64 coded pieces (benches/full_rlnc_encoder.rs:111-113) + k·(k+L) for the decode
+(benches/full_rlnc_decoder.rs:118), summed over all ranks, ÷ the max-over-ranks wall time of the timed steps.
+Multi-GPU: objects are sharded across ranks (weak scaling), no data-path collective; the only collectives
+are the timing barrier and the max/sum reductions of the result.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident RLNC encode+decode GiB/s, k=32 × 1 MiB, at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GIB = float(1 << 30)
+
+
+def encode_counter(k: int, L: int) -> int:
+    """Bytes per coded piece, benches/full_rlnc_encoder.rs:111-113."""
+    return k * L + k + L
+
+
+def decode_counter(k: int, L: int) -> int:
+    """Bytes per decoded object, benches/full_rlnc_decoder.rs:118."""
+    return k * (k + L)
+
+
+def step_bytes(objects: int, k: int, L: int, n: int) -> int:
+    return objects * (n * encode_counter(k, L) + decode_counter(k, L))
+
+
+# ------------------------------------------------------------------------------------------------------
+# distributed timing harness (CPU-testable with gloo: tests/test_distributed.py)
+# ------------------------------------------------------------------------------------------------------
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+
+    def init(self, backend: str):
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.init_process_group(backend=backend)
+            self.pg = dist
+        return self
+
+    def barrier(self):
+        if self.pg:
+            self.pg.barrier()
+
+    def allreduce(self, value: float, op: str) -> float:
+        if not self.pg:
+            return value
+        import torch
+
+        dev = "cuda" if self.pg.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([value], dtype=torch.float64, device=dev)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX if op == "max" else self.pg.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.pg:
+            self.pg.destroy_process_group()
+
+
+def timed_loop(step, steps: int, warmup: int, dist: Dist, sync) -> float:
+    """W untimed steps, then exactly K steps bracketed by barrier + device sync; returns max-over-ranks s."""
+    for _ in range(warmup):
+        step()
+    sync()
+    dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    return dist.allreduce(elapsed, "max")
+
+
+# ------------------------------------------------------------------------------------------------------
+# CPU baseline: the oracle (C restatement of the reference's algorithm) — "port"
+# ------------------------------------------------------------------------------------------------------
+def cpu_model() -> str:
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(k: int, L: int, n: int, m: int, seconds: float) -> dict:
+    """Reference algorithm on the host (single thread): encode n coded pieces of one object
+    (encoder.rs:128-144 per piece) + decode m of them with a full-row RREF per piece
+    (decoder.rs:96-118), repeated until `seconds` of CPU work; same byte counters as the GPU value."""
+    import numpy as np
+
+    from oracle.oracle import Oracle, OracleDecoder
+
+    orc = Oracle()
+    rng = np.random.default_rng(0x524C4E43)
+    src = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    coeffs = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    iters = 0
+    t0 = time.perf_counter()
+    while True:
+        coded = orc.encode(src, coeffs)
+        dec = OracleDecoder(L, k)
+        for p in coded[:m]:
+            dec.decode(p)
+        dec.get_decoded_data()
+        iters += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    value = iters * (n * encode_counter(k, L) + decode_counter(k, L)) / el / GIB
+    return {
+        "value": round(value, 4),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{iters} x (1 object k={k} L={L}: encode {n} coded pieces + decode {m} with per-piece "
+                  f"full-row RREF), {el:.1f} s, single thread, oracle/liboracle.so ({orc.simd_variant()}) "
+                  f"on {cpu_model()}",
+    }
+
+
+# ------------------------------------------------------------------------------------------------------
+# GPU run
+# ------------------------------------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--objects", type=int, default=16, help="objects per GPU per step")
+    ap.add_argument("--k", type=int, default=32)
+    ap.add_argument("--piece-bytes", type=int, default=1 << 20)
+    ap.add_argument("--coded", type=int, default=64)
+    ap.add_argument("--decode-from", type=int, default=32)
+    ap.add_argument("--variant", type=int, default=0, help="0 perm (v_perm_b32), 1 nibble-LDS")
+    ap.add_argument("--tile-rows", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--encode-only", action="store_true", help="diagnostic: time only the encode launch")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    dist = Dist()
+    assert dist.world == args.gpus or (dist.world == 1 and args.gpus == 1), \
+        f"--gpus {args.gpus} but WORLD_SIZE={dist.world} (launch with torch.distributed.run for N>1)"
+    torch.cuda.set_device(dist.local_rank)
+    dist.init("nccl")
+
+    import rlnc_amd
+    from rlnc_amd import batch
+
+    k, L, n, m, B = args.k, args.piece_bytes, args.coded, args.decode_from, args.objects
+    ctx = rlnc_amd.Context(dist.local_rank)
+    ctx.set_kernel_variant(args.variant, args.tile_rows)
+    dev = torch.device("cuda", dist.local_rank)
+
+    # synthetic objects of the named shape, generated on device; coefficients from a host RNG (like
+    # rng.fill_bytes in the reference) and uploaded before timing
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0x524C4E43 + dist.rank)
+    src = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=gen)
+    coeffs = torch.from_numpy(np.random.default_rng(1000 + dist.rank).integers(0, 256, (B, n, k), dtype=np.uint8)).to(dev)
+    pieces = torch.empty((B, n, k + L), dtype=torch.uint8, device=dev)
+    decoded = torch.empty((B, k, L), dtype=torch.uint8, device=dev)
+    received = pieces[:, :m]
+
+    enc_events = []
+    dec_wall = []
+
+    def step():
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        batch.encode_batch(src, coeffs, pieces, ctx)
+        e1.record()
+        enc_events.append((e0, e1))
+        if not args.encode_only:
+            t = time.perf_counter()
+            batch.decode_batch(received, k, decoded, ctx)
+            dec_wall.append(time.perf_counter() - t)
+
+    elapsed = timed_loop(step, args.steps, args.warmup, dist, torch.cuda.synchronize)
+    torch.cuda.synchronize()
+    timed_enc = enc_events[args.warmup:]
+    enc_ms = sum(a.elapsed_time(b) for a, b in timed_enc) / len(timed_enc)
+    dec_ms = 1e3 * sum(dec_wall[args.warmup:]) / max(1, len(dec_wall[args.warmup:]))
+
+    # correctness of what was timed: statuses + decoded == source for every full-rank object
+    ok = True
+    if not args.encode_only:
+        pst, ost, _ = batch.decode_batch(received, k, decoded, ctx)
+        torch.cuda.synchronize()
+        for o in range(B):
+            if (pst[o] == 0).sum() == k and not torch.equal(decoded[o], src[o]):
+                ok = False
+        ok = ok and bool((pst == 0).sum(axis=1).max() == k)
+
+    per_rank_bytes = step_bytes(B, k, L, n) if not args.encode_only else B * n * encode_counter(k, L)
+    total_bytes = dist.allreduce(float(per_rank_bytes * args.steps), "sum")
+    value = total_bytes / elapsed / GIB
+
+    # roofline of the dominant kernel (the encode matmul, one launch per step) from HIP events
+    enc_alg = B * n * encode_counter(k, L)           # reference counter bytes per launch
+    enc_compulsory = B * (k * L + n * (k + L))       # source read once + coded pieces written
+    achieved = enc_alg / (enc_ms * 1e-3) / 1e9
+    ma_per_launch = B * n * k * L                    # GF(2^8) multiply-adds per launch
+    roofline = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "kernel": "gf_matmul_perm_kernel<32,true> (encode: 64 coded pieces x 16 objects per launch)",
+        "kernel_ms": round(enc_ms, 4),
+        "outputs_per_pass": n,
+        "compulsory_bytes": enc_compulsory,
+        "compulsory_GBps": round(enc_compulsory / (enc_ms * 1e-3) / 1e9, 1),
+        "compulsory_frac": round(enc_compulsory / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "gf_muladd_per_s": round(ma_per_launch / (enc_ms * 1e-3) / 1e12, 3),
+        "gf_muladd_unit": "T byte-multiply-adds/s",
+    }
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": dist.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: uniform random source bytes (torch generator, seeded per rank), coefficients "
+                "uniform bytes from a seeded host RNG",
+        "config": {
+            "workload": f"per object: encode k={k} x {L} B -> {n} coded pieces (configs[1]) + decode from the "
+                        f"first {m} (configs[2]); {B} objects per GPU per step",
+            "k": k, "piece_bytes": L, "coded_per_object": n, "decoded_from": m, "objects_per_gpu": B,
+            "parallelism": f"objects sharded over {dist.world} rank(s), no data-path collective",
+            "kernel_variant": ["perm", "nibble"][args.variant],
+        },
+        "roofline": roofline,
+        "cpu_baseline": None,
+        "breakdown": {
+            "encode_kernel_ms": round(enc_ms, 4),
+            "decode_call_ms": round(dec_ms, 4),
+            "encode_GiBps_refcounter": round(B * n * encode_counter(k, L) / (enc_ms * 1e-3) / GIB, 1),
+            "decode_GiBps_refcounter": round(B * decode_counter(k, L) / (dec_ms * 1e-3) / GIB, 2) if dec_ms else None,
+            "roundtrip_goodput_GiBps": round(dist.world * B * k * L * args.steps / elapsed / GIB, 2),
+            "verified": ok,
+        },
+    }
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(k, L, n, m, args.cpu_seconds)
+        result["vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
+    if dist.rank == 0:
+        print(json.dumps(result), flush=True)
+    dist.close()
+    if not ok:
+        print("VERIFICATION FAILED: decoded data does not match the source", file=sys.stderr)
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,208 @@
+/*
+ * rlnc_hip.h — C ABI of librlnc_hip.so, the MI355X (gfx950) engine for the RLNC hot path of
+ * itzmeanjan/rlnc 0.8.5.
+ *
+ * Drop-in boundary.  The reference exposes exactly three types plus one error enum
+ * (rlnc::full::{Encoder, Decoder, Recoder}, rlnc::RLNCError — src/lib.rs:127-130, src/full/mod.rs:9-11);
+ * its internal seam is the three src/common/simd functions (simd/mod.rs:18,58,89).  Every entry point
+ * below names the reference item it replaces.  The Rust-side binding a maintainer would add is in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *   - Plain C: pointers + sizes, no exceptions across the ABI, no torch types.
+ *   - Return value: RLNC_OK (0) or a status code.  Codes 1..13 are RLNCError discriminant + 1
+ *     (src/common/errors.rs:3-32, same order); >= 100 are engine/device errors (rlnc_last_error() has
+ *     the message, thread-local).
+ *   - Randomness stays with the caller (the reference draws coefficients with rng.fill_bytes,
+ *     encoder.rs:248 / recoder.rs:131): functions that the reference feeds from an RNG take those
+ *     bytes explicitly, so outputs are bit-exact given the same coefficient bytes.
+ *   - "_device" / batch functions take device pointers (hipMalloc'd memory on the context's device) and
+ *     are asynchronous on the context's stream; the object API (encoder/decoder/recoder on host buffers)
+ *     is synchronous, like the Rust API it mirrors.
+ *   - One context per host thread (mirrors &mut self of Decoder/Recoder); objects are bound to the
+ *     context that created them.
+ */
+#ifndef RLNC_HIP_H
+#define RLNC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes: errors.rs:3-32 (discriminant + 1) ------------------------------------------- */
+#define RLNC_OK 0
+#define RLNC_ERR_CODING_VECTOR_LENGTH_MISMATCH 1 /* errors.rs:6  */
+#define RLNC_ERR_DATA_LENGTH_MISMATCH 2          /* errors.rs:8  */
+#define RLNC_ERR_PIECE_COUNT_ZERO 3              /* errors.rs:10 */
+#define RLNC_ERR_DATA_LENGTH_ZERO 4              /* errors.rs:12 */
+#define RLNC_ERR_PIECE_LENGTH_ZERO 5             /* errors.rs:14 */
+#define RLNC_ERR_NOT_ENOUGH_PIECES_TO_RECODE 6   /* errors.rs:17 */
+#define RLNC_ERR_PIECE_LENGTH_TOO_SHORT 7        /* errors.rs:19 */
+#define RLNC_ERR_PIECE_NOT_USEFUL 8              /* errors.rs:22 */
+#define RLNC_ERR_RECEIVED_ALL_PIECES 9           /* errors.rs:24 */
+#define RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET 10  /* errors.rs:26 */
+#define RLNC_ERR_INVALID_DECODED_DATA_FORMAT 11  /* errors.rs:28 */
+#define RLNC_ERR_INVALID_PIECE_LENGTH 12         /* errors.rs:30 */
+#define RLNC_ERR_INVALID_OUTPUT_BUFFER 13        /* errors.rs:31 */
+/* engine errors (no reference counterpart) */
+#define RLNC_ERR_INVALID_ARGUMENT 100 /* null handle/pointer, size overflow, misuse of the ABI */
+#define RLNC_ERR_DEVICE 101           /* HIP runtime / launch failure */
+#define RLNC_ERR_OUT_OF_MEMORY 102    /* device or pinned-host allocation failed */
+#define RLNC_ERR_NO_DEVICE 103        /* no usable gfx950 device */
+
+const char *rlnc_status_name(int status); /* "Ok", "PieceNotUseful", ... (errors.rs:34-58 variant names) */
+const char *rlnc_status_message(int status); /* Display text, errors.rs:34-58 */
+const char *rlnc_last_error(void);        /* detail of the last engine error on this thread */
+const char *rlnc_version(void);
+
+/* ---- context: device + HIP stream + workspace ----------------------------------------------------- */
+typedef struct rlnc_context rlnc_context;
+int rlnc_context_create(int device, rlnc_context **out);
+void rlnc_context_destroy(rlnc_context *ctx);
+/* Use an external hipStream_t (NULL = the context's own stream).  The caller keeps ownership. */
+int rlnc_context_set_stream(rlnc_context *ctx, void *hip_stream);
+void *rlnc_context_get_stream(rlnc_context *ctx);
+int rlnc_context_synchronize(rlnc_context *ctx);
+int rlnc_context_device(const rlnc_context *ctx);
+
+/* ---- L1: vector primitives on device buffers (src/common/simd/mod.rs) --------------------------------
+ * Same scalar early-outs as the reference (0 → zero-fill / no-op, 1 → no-op / plain XOR). */
+int rlnc_gf256_inplace_mul_vec_by_scalar(rlnc_context *ctx, uint8_t *vec_dev, size_t len, uint8_t scalar); /* :18-47 */
+int rlnc_gf256_inplace_add_vectors(rlnc_context *ctx, uint8_t *dst_dev, const uint8_t *src_dev, size_t len); /* :58-76 */
+int rlnc_gf256_mul_vec_by_scalar_then_add_into_vec(rlnc_context *ctx, uint8_t *dst_dev, const uint8_t *src_dev,
+                                                   size_t len, uint8_t scalar); /* :89-119 */
+
+/* ---- L2: the matrix-level hot operator (device buffers) -----------------------------------------------
+ * out[o][i][0:width) = XOR_j coef[o][i][j] · in[o][j][0:width)   (i < n_out, j < n_in, o < n_obj)
+ * Replaces the loop of gf256_mul_vec_by_scalar_then_add_into_vec calls in
+ * Encoder::code_with_coding_vector (encoder.rs:138-141), batched over n_out coding vectors and n_obj
+ * independent objects.  All strides in bytes.  hdr (optional, may be NULL) also receives the coefficient
+ * rows, hdr[o][i][0:n_in) — the coeffs‖data framing of a full coded piece (encoder.rs:246-248). */
+typedef struct rlnc_matmul_desc {
+    const uint8_t *in;
+    int64_t in_obj_stride, in_row_stride;
+    const uint8_t *coef;
+    int64_t coef_obj_stride, coef_row_stride;
+    uint8_t *out;
+    int64_t out_obj_stride, out_row_stride;
+    uint8_t *hdr;
+    int64_t hdr_obj_stride, hdr_row_stride;
+    int32_t n_out, n_in;
+    int64_t width;
+    int32_t n_obj;
+} rlnc_matmul_desc;
+int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc);
+/* Kernel variant for A/B measurement: 0 = perm (3-bit split tables in LDS consumed by v_perm_b32,
+ * default), 1 = nibble (the reference's 4-bit split LOW/HIGH tables looked up from LDS byte-wise).
+ * max_tile_rows caps the output rows per workgroup (0 = automatic, else 1/2/4/8/16/32). */
+int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows);
+
+/* ---- Encoder: src/full/encoder.rs ----------------------------------------------------------------- */
+typedef struct rlnc_encoder rlnc_encoder;
+/* Encoder::new (encoder.rs:85-106): pads with the 0x81 marker + zeros; data is host memory (copied). */
+int rlnc_encoder_new(rlnc_context *ctx, const uint8_t *data, size_t data_len, size_t piece_count, rlnc_encoder **out);
+/* Encoder::without_padding (encoder.rs:50-71). */
+int rlnc_encoder_without_padding(rlnc_context *ctx, const uint8_t *data, size_t data_len, size_t piece_count,
+                                 rlnc_encoder **out);
+/* Device-resident source: piece_count rows of piece_len bytes at row_stride (borrowed, not copied; must
+ * outlive the encoder). */
+int rlnc_encoder_from_device(rlnc_context *ctx, const uint8_t *pieces_dev, size_t piece_count, size_t piece_len,
+                             size_t row_stride, rlnc_encoder **out);
+void rlnc_encoder_free(rlnc_encoder *enc);
+size_t rlnc_encoder_get_piece_count(const rlnc_encoder *enc);              /* encoder.rs:27-29 */
+size_t rlnc_encoder_get_piece_byte_len(const rlnc_encoder *enc);           /* encoder.rs:32-34 */
+size_t rlnc_encoder_get_full_coded_piece_byte_len(const rlnc_encoder *enc); /* encoder.rs:37-39 */
+/* Encoder::code_with_coding_vector (encoder.rs:128-144), host buffers. */
+int rlnc_encoder_code_with_coding_vector(rlnc_encoder *enc, const uint8_t *coding_vector, size_t cv_len,
+                                         uint8_t *coded_data, size_t coded_len);
+/* Encoder::code_with_buf (encoder.rs:241-250): random_bytes are the piece_count bytes rng.fill_bytes
+ * would have written into the coefficient prefix (n_random must equal piece_count, else
+ * CodingVectorLengthMismatch); the output length is checked first, like the reference. */
+int rlnc_encoder_code_with_buf(rlnc_encoder *enc, const uint8_t *random_bytes, size_t n_random,
+                               uint8_t *full_coded_piece, size_t full_len);
+/* n coded pieces in one launch, device buffers: coeffs_dev [n][k] → out_dev [n][k+L] (coeffs‖data,
+ * row stride out_row_stride >= k+L; pass 0 for k+L). */
+int rlnc_encoder_code_batch_device(rlnc_encoder *enc, const uint8_t *coeffs_dev, size_t n, uint8_t *out_dev,
+                                   size_t out_row_stride);
+
+/* ---- Recoder: src/full/recoder.rs ---------------------------------------------------------------- */
+typedef struct rlnc_recoder rlnc_recoder;
+/* Recoder::new (recoder.rs:68-108); data = concatenated full coded pieces (host, copied). */
+int rlnc_recoder_new(rlnc_context *ctx, const uint8_t *data, size_t data_len, size_t full_coded_piece_byte_len,
+                     size_t num_pieces_coded_together, rlnc_recoder **out);
+void rlnc_recoder_free(rlnc_recoder *rec);
+size_t rlnc_recoder_get_original_num_pieces_coded_together(const rlnc_recoder *rec); /* recoder.rs:26-28 */
+size_t rlnc_recoder_get_num_pieces_recoded_together(const rlnc_recoder *rec);       /* recoder.rs:31-33 */
+size_t rlnc_recoder_get_piece_byte_len(const rlnc_recoder *rec);                    /* recoder.rs:36-38 */
+size_t rlnc_recoder_get_full_coded_piece_byte_len(const rlnc_recoder *rec);         /* recoder.rs:41-43 */
+/* Recoder::recode_with_buf (recoder.rs:122-153): random_bytes = the n recoding coefficients that
+ * rng.fill_bytes would have drawn (n_random must equal n, else CodingVectorLengthMismatch). */
+int rlnc_recoder_recode_with_buf(rlnc_recoder *rec, const uint8_t *random_bytes, size_t n_random,
+                                 uint8_t *full_recoded_piece, size_t full_len);
+/* count recoded pieces in one launch: r_dev [count][n] → out_dev [count][k+L] (device). */
+int rlnc_recoder_recode_batch_device(rlnc_recoder *rec, const uint8_t *r_dev, size_t count, uint8_t *out_dev);
+
+/* ---- Decoder: src/full/decoder.rs ----------------------------------------------------------------- */
+typedef struct rlnc_decoder rlnc_decoder;
+/* Decoder::new(piece_byte_len, required_piece_count) (decoder.rs:65-80; note the argument order). */
+int rlnc_decoder_new(rlnc_context *ctx, size_t piece_byte_len, size_t required_piece_count, rlnc_decoder **out);
+void rlnc_decoder_free(rlnc_decoder *dec);
+/* Decoder::decode (decoder.rs:96-118): Ok / PieceNotUseful / ReceivedAllPieces / InvalidPieceLength.
+ * The accept/reject answer is immediate (exact replica of the diagonal-pivot RREF on the coefficient
+ * block); the data rows are combined on the device when the data is requested. */
+int rlnc_decoder_decode(rlnc_decoder *dec, const uint8_t *full_coded_piece, size_t len);
+/* Same, piece already in HBM (only its k coefficient bytes are read back to the host). */
+int rlnc_decoder_decode_device(rlnc_decoder *dec, const uint8_t *piece_dev, size_t len);
+int rlnc_decoder_is_already_decoded(const rlnc_decoder *dec);                   /* decoder.rs:121-123 */
+size_t rlnc_decoder_get_num_pieces_coded_together(const rlnc_decoder *dec);     /* decoder.rs:25-27 */
+size_t rlnc_decoder_get_piece_byte_len(const rlnc_decoder *dec);                /* decoder.rs:30-32 */
+size_t rlnc_decoder_get_full_coded_piece_byte_len(const rlnc_decoder *dec);     /* decoder.rs:35-37 */
+size_t rlnc_decoder_get_received_piece_count(const rlnc_decoder *dec);          /* decoder.rs:40-42 */
+size_t rlnc_decoder_get_useful_piece_count(const rlnc_decoder *dec);            /* decoder.rs:45-47 */
+size_t rlnc_decoder_get_remaining_piece_count(const rlnc_decoder *dec);         /* decoder.rs:50-52 */
+/* Decoder::get_decoded_data (decoder.rs:136-177) into host memory: out must hold k*L bytes (the padded
+ * size); *out_len receives the unpadded length.  Does not consume the decoder (the C caller frees it). */
+int rlnc_decoder_get_decoded_data(rlnc_decoder *dec, uint8_t *out, size_t out_cap, size_t *out_len);
+/* Same into device memory (out_dev holds k*L bytes). */
+int rlnc_decoder_get_decoded_data_device(rlnc_decoder *dec, uint8_t *out_dev, size_t out_cap, size_t *out_len);
+
+/* ---- multi-object batch API (device-resident) -------------------------------
+ * Layouts (bytes, contiguous): src [obj][k][L]; coeffs [obj][n][k]; pieces [obj][n][k+L] (coeffs‖data). */
+/* n coded pieces for each of num_objects objects (encoder.rs:241-250 × n × objects). */
+int rlnc_encode_batch(rlnc_context *ctx, const uint8_t *src_dev, size_t k, size_t L, size_t num_objects,
+                      const uint8_t *coeffs_dev, size_t n, uint8_t *pieces_dev);
+/* count recoded pieces per object from n received pieces: r [obj][count][n] → out [obj][count][k+L]
+ * (recoder.rs:122-153; coefficient header and data are one linear combination of the full pieces). */
+int rlnc_recode_batch(rlnc_context *ctx, const uint8_t *pieces_dev, size_t k, size_t L, size_t n,
+                      size_t num_objects, const uint8_t *r_dev, size_t count, uint8_t *out_dev);
+/* Feeds pieces 0..m-1 of every object, in order, to a fresh Decoder (decoder.rs:96-118) and extracts the
+ * data (decoder.rs:136-177).  decoded_dev [obj][k][L] receives the padded payload rows in the reference's
+ * row order.  pieces_obj_stride = bytes between objects' first pieces (0 = m*(k+L), i.e. dense; a larger
+ * stride decodes from the first m of more coded pieces in place).  Host outputs (each may be NULL): piece_status [obj][m] (status of each decode() call),
+ * object_status [obj] (Ok / NotAllPiecesReceivedYet / InvalidDecodedDataFormat of get_decoded_data),
+ * data_len [obj] (unpadded length when Ok).  Synchronous. */
+int rlnc_decode_batch(rlnc_context *ctx, const uint8_t *pieces_dev, size_t pieces_obj_stride, size_t k, size_t L,
+                      size_t m, size_t num_objects, uint8_t *decoded_dev, int32_t *piece_status,
+                      int32_t *object_status, uint64_t *data_len);
+
+/* ---- host-only: the decoder's exact coefficient elimination (no device needed) ---------------------------
+ * The diagonal-pivot RREF of DecoderMatrix (decoder_matrix.rs:99-244) replicated on [coeffs | E] where E
+ * tracks every row as a combination of received pieces; data rows = E × received data (elimination.hpp).
+ * fixed_slots > 0: piece p owns E column p; 0: columns are recycled once unreferenced. */
+typedef struct rlnc_elimination rlnc_elimination;
+int rlnc_elimination_new(size_t k, size_t fixed_slots, rlnc_elimination **out);
+void rlnc_elimination_free(rlnc_elimination *e);
+/* Decoder::decode on the k coefficient bytes: Ok / PieceNotUseful / ReceivedAllPieces. */
+int rlnc_elimination_push(rlnc_elimination *e, const uint8_t *coeffs, int32_t *slot, int32_t *keep);
+size_t rlnc_elimination_rank(const rlnc_elimination *e);
+size_t rlnc_elimination_slots(const rlnc_elimination *e);
+int rlnc_elimination_transform(const rlnc_elimination *e, uint8_t *T, size_t ld); /* k × ld, zero-filled */
+int rlnc_elimination_coefficients(const rlnc_elimination *e, uint8_t *C);        /* rank × k */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RLNC_HIP_H */

@@ -1,0 +1,118 @@
+"""Multi-object, device-resident batch API on torch tensors (torch is plumbing: HBM + streams only).
+
+Layouts (uint8, contiguous, on the context's device):
+    src     [obj][k][L]          source pieces (Encoder::new's padded image per object)
+    coeffs  [obj][n][k]          coding vectors
+    pieces  [obj][n][k+L]        full coded pieces, coeffs ‖ data (encoder.rs:246-248)
+    decoded [obj][k][L]          padded payload rows (decoder.rs:141-153)
+All launches go to torch's current stream of the tensors' device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import MatmulDesc
+from .context import Context, default_context
+from .errors import check
+
+
+def _ctx_for(t, ctx: Context | None) -> Context:
+    ctx = ctx or default_context(t.device.index or 0)
+    ctx.use_torch_stream()
+    return ctx
+
+
+def _chk(t, shape=None):
+    import torch
+
+    assert t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous(), "uint8 contiguous device tensor required"
+    if shape is not None:
+        assert tuple(t.shape) == tuple(shape), (tuple(t.shape), shape)
+
+
+def encode_batch(src, coeffs, out, ctx: Context | None = None) -> None:
+    """out[o][i] = coeffs[o][i] ‖ Σ_j coeffs[o][i][j]·src[o][j]  (n coded pieces per object)."""
+    nobj, k, L = src.shape
+    n = coeffs.shape[1]
+    _chk(src)
+    _chk(coeffs, (nobj, n, k))
+    _chk(out, (nobj, n, k + L))
+    ctx = _ctx_for(src, ctx)
+    check(ctx.lib.rlnc_encode_batch(ctx.h, C.c_void_p(src.data_ptr()), k, L, nobj, C.c_void_p(coeffs.data_ptr()), n,
+                                    C.c_void_p(out.data_ptr())), ctx.lib)
+
+
+def recode_batch(pieces, r, out, k: int, ctx: Context | None = None) -> None:
+    """out[o][c] = Σ_i r[o][c][i]·pieces[o][i] (coefficient header and data alike, recoder.rs:122-153)."""
+    nobj, n, full = pieces.shape
+    count = r.shape[1]
+    _chk(pieces)
+    _chk(r, (nobj, count, n))
+    _chk(out, (nobj, count, full))
+    ctx = _ctx_for(pieces, ctx)
+    check(ctx.lib.rlnc_recode_batch(ctx.h, C.c_void_p(pieces.data_ptr()), k, full - k, n, nobj,
+                                    C.c_void_p(r.data_ptr()), count, C.c_void_p(out.data_ptr())), ctx.lib)
+
+
+def decode_batch(pieces, k: int, decoded, ctx: Context | None = None):
+    """Feed pieces[o][0..m) to a fresh Decoder per object; returns (piece_status[obj][m],
+    object_status[obj], data_len[obj]) as numpy arrays (status codes: rlnc_amd.errors.STATUS_NAMES).
+    `pieces` may be a view pieces_all[:, :m] of more coded pieces (rows contiguous, objects strided)."""
+    import torch
+
+    nobj, m, full = pieces.shape
+    L = full - k
+    assert pieces.is_cuda and pieces.dtype == torch.uint8
+    assert pieces.stride(2) == 1 and pieces.stride(1) == full and pieces.stride(0) >= m * full
+    _chk(decoded, (nobj, k, L))
+    ctx = _ctx_for(pieces, ctx)
+    ps = np.zeros((nobj, m), np.int32)
+    os_ = np.zeros(nobj, np.int32)
+    dl = np.zeros(nobj, np.uint64)
+    check(ctx.lib.rlnc_decode_batch(ctx.h, C.c_void_p(pieces.data_ptr()), pieces.stride(0), k, L, m, nobj,
+                                    C.c_void_p(decoded.data_ptr()),
+                                    ps.ctypes.data_as(C.POINTER(C.c_int32)), os_.ctypes.data_as(C.POINTER(C.c_int32)),
+                                    dl.ctypes.data_as(C.POINTER(C.c_uint64))), ctx.lib)
+    return ps, os_, dl
+
+
+def matmul(coef, inp, out, ctx: Context | None = None) -> None:
+    """out[o] = coef[o] ⊗ inp[o] over GF(2^8); coef [obj][n_out][n_in], inp [obj][n_in][W], out [obj][n_out][W]."""
+    nobj, n_out, n_in = coef.shape
+    W = inp.shape[2]
+    _chk(coef)
+    _chk(inp, (nobj, n_in, W))
+    _chk(out, (nobj, n_out, W))
+    ctx = _ctx_for(inp, ctx)
+    d = MatmulDesc(inp.data_ptr(), n_in * W, W, coef.data_ptr(), n_out * n_in, n_in, out.data_ptr(), n_out * W, W,
+                   None, 0, 0, n_out, n_in, W, nobj)
+    check(ctx.lib.rlnc_gf256_matmul(ctx.h, C.byref(d)), ctx.lib)
+
+
+def mul_vec_by_scalar(vec, scalar: int, ctx: Context | None = None) -> None:
+    """gf256_inplace_mul_vec_by_scalar (simd/mod.rs:18-47) on a device vector."""
+    _chk(vec)
+    ctx = _ctx_for(vec, ctx)
+    check(ctx.lib.rlnc_gf256_inplace_mul_vec_by_scalar(ctx.h, C.c_void_p(vec.data_ptr()), vec.numel(), scalar),
+          ctx.lib)
+
+
+def add_vectors(dst, src, ctx: Context | None = None) -> None:
+    """gf256_inplace_add_vectors (simd/mod.rs:58-76)."""
+    _chk(dst)
+    _chk(src, tuple(dst.shape))
+    ctx = _ctx_for(dst, ctx)
+    check(ctx.lib.rlnc_gf256_inplace_add_vectors(ctx.h, C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()),
+                                                 dst.numel()), ctx.lib)
+
+
+def mul_vec_by_scalar_then_add_into_vec(dst, src, scalar: int, ctx: Context | None = None) -> None:
+    """gf256_mul_vec_by_scalar_then_add_into_vec (simd/mod.rs:89-119)."""
+    _chk(dst)
+    _chk(src, tuple(dst.shape))
+    ctx = _ctx_for(dst, ctx)
+    check(ctx.lib.rlnc_gf256_mul_vec_by_scalar_then_add_into_vec(ctx.h, C.c_void_p(dst.data_ptr()),
+                                                                 C.c_void_p(src.data_ptr()), dst.numel(), scalar),
+          ctx.lib)

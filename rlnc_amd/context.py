@@ -1,0 +1,60 @@
+"""Device context (device + HIP stream + workspace) of librlnc_hip."""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+
+from . import _lib
+from .errors import RLNCError, check
+
+_tls = threading.local()
+
+
+class Context:
+    """Owns an rlnc_context (one per host thread, like the reference's &mut self types)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        h = C.c_void_p()
+        check(self.lib.rlnc_context_create(int(device), C.byref(h)), self.lib)
+        self.h = h
+        self.device = int(device)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.rlnc_context_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, hip_stream_handle: int | None):
+        """Launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""
+        check(self.lib.rlnc_context_set_stream(self.h, C.c_void_p(hip_stream_handle or 0)), self.lib)
+
+    def use_torch_stream(self):
+        import torch
+
+        self.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def synchronize(self):
+        check(self.lib.rlnc_context_synchronize(self.h), self.lib)
+
+    def set_kernel_variant(self, variant: int = 0, max_tile_rows: int = 0):
+        """variant 0 = perm (v_perm_b32 3-bit split, default), 1 = nibble (4-bit LDS tables)."""
+        check(self.lib.rlnc_set_kernel_variant(self.h, int(variant), int(max_tile_rows)), self.lib)
+
+
+def default_context(device: int = 0) -> Context:
+    ctxs = getattr(_tls, "ctxs", None)
+    if ctxs is None:
+        ctxs = _tls.ctxs = {}
+    if device not in ctxs:
+        ctxs[device] = Context(device)
+    return ctxs[device]
+
+
+__all__ = ["Context", "default_context", "RLNCError"]

@@ -1,0 +1,924 @@
+// engine.cpp — librlnc_hip: context, Encoder / Recoder / Decoder objects and the batch API behind the
+// C ABI of include/rlnc_hip.h.  Mirrors rlnc::full::{Encoder, Recoder, Decoder} (src/full/*.rs):
+// same constructor validation order, same status for every error, same getters.  All GF(2^8) byte work on
+// pieces runs on the device through the kernels of kernels.hip; the host only runs the k×(k+slots)
+// coefficient elimination of the decoder (elimination.hpp).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/rlnc_hip.h"
+#include "elimination.hpp"
+#include "gf256.hpp"
+#include "kernels.hpp"
+
+using rlnc::Elimination;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                    \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess) {                                                                          \
+            return set_error(e_ == hipErrorOutOfMemory ? RLNC_ERR_OUT_OF_MEMORY : RLNC_ERR_DEVICE,       \
+                             "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+        }                                                                                                \
+    } while (0)
+
+#define CHECK_ARG(cond)                                                                         \
+    do {                                                                                        \
+        if (!(cond)) return set_error(RLNC_ERR_INVALID_ARGUMENT, "invalid argument: %s", #cond); \
+    } while (0)
+
+inline size_t round16(size_t v) { return (v + 15) & ~size_t(15); }
+
+// grow-only device buffer
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return RLNC_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        HIP_TRY(hipMalloc(&p, std::max<size_t>(bytes, 256)));
+        cap = std::max<size_t>(bytes, 256);
+        return RLNC_OK;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    template <class T>
+    T *as() const {
+        return static_cast<T *>(p);
+    }
+};
+
+// grow-only pinned host buffer
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return RLNC_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        HIP_TRY(hipHostMalloc(&p, std::max<size_t>(bytes, 256), hipHostMallocDefault));
+        cap = std::max<size_t>(bytes, 256);
+        return RLNC_OK;
+    }
+    ~PinBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    template <class T>
+    T *as() const {
+        return static_cast<T *>(p);
+    }
+};
+
+}  // namespace
+
+struct rlnc_context {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    rlnc::MatmulVariant variant = rlnc::MatmulVariant::Perm;
+    int max_tile_rows = 0;
+    DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len;
+    PinBuf pin_a, pin_b, pin_c;
+
+    int activate() const {
+        HIP_TRY(hipSetDevice(device));
+        return RLNC_OK;
+    }
+    int matmul(rlnc::MatmulParams p) {
+        if (max_tile_rows > 0 && p.n_out > max_tile_rows) {
+            // split the output rows into launches of at most max_tile_rows rows (tuning knob)
+            const int total = p.n_out;
+            for (int r0 = 0; r0 < total; r0 += max_tile_rows) {
+                rlnc::MatmulParams q = p;
+                q.n_out = std::min(max_tile_rows, total - r0);
+                q.coef = p.coef + int64_t(r0) * p.coef_row;
+                q.out = p.out + int64_t(r0) * p.out_row;
+                if (p.hdr) q.hdr = p.hdr + int64_t(r0) * p.hdr_row;
+                HIP_TRY(rlnc::launch_matmul(q, stream, variant));
+            }
+            return RLNC_OK;
+        }
+        HIP_TRY(rlnc::launch_matmul(p, stream, variant));
+        return RLNC_OK;
+    }
+};
+
+struct rlnc_encoder {
+    rlnc_context *ctx;
+    size_t k, L, stride;
+    uint8_t *src = nullptr;  // k rows × stride
+    bool owned = false;
+    ~rlnc_encoder() {
+        if (owned && src) (void)hipFree(src);
+    }
+};
+
+struct rlnc_recoder {
+    rlnc_context *ctx;
+    size_t k, n, full, stride;
+    uint8_t *pieces = nullptr;  // n rows × stride (coeffs ‖ data)
+    ~rlnc_recoder() {
+        if (pieces) (void)hipFree(pieces);
+    }
+};
+
+struct rlnc_decoder {
+    rlnc_context *ctx;
+    size_t k, L, stride;
+    size_t received = 0, useful = 0;
+    std::unique_ptr<Elimination> elim;
+    uint8_t *store = nullptr;  // slot rows × stride (received data rows still referenced by E)
+    size_t store_slots = 0;
+    ~rlnc_decoder() {
+        if (store) (void)hipFree(store);
+    }
+};
+
+namespace {
+
+int matmul_desc_to_params(const rlnc_matmul_desc *d, rlnc::MatmulParams &p) {
+    p.in = d->in;
+    p.in_obj = d->in_obj_stride;
+    p.in_row = d->in_row_stride;
+    p.coef = d->coef;
+    p.coef_obj = d->coef_obj_stride;
+    p.coef_row = d->coef_row_stride;
+    p.out = d->out;
+    p.out_obj = d->out_obj_stride;
+    p.out_row = d->out_row_stride;
+    p.hdr = d->hdr;
+    p.hdr_obj = d->hdr_obj_stride;
+    p.hdr_row = d->hdr_row_stride;
+    p.n_out = d->n_out;
+    p.n_in = d->n_in;
+    p.width = d->width;
+    p.n_obj = d->n_obj;
+    return RLNC_OK;
+}
+
+// One coded piece on the device: out_dev[0:L) = Σ_j cv[j] · src_j  (cv already on the device)
+int encoder_launch(rlnc_encoder *e, const uint8_t *cv_dev, int64_t cv_row, int n, uint8_t *out_dev, int64_t out_row,
+                   uint8_t *hdr_dev, int64_t hdr_row) {
+    rlnc::MatmulParams p{};
+    p.in = e->src;
+    p.in_row = int64_t(e->stride);
+    p.coef = cv_dev;
+    p.coef_row = cv_row;
+    p.out = out_dev;
+    p.out_row = out_row;
+    p.hdr = hdr_dev;
+    p.hdr_row = hdr_row;
+    p.n_out = n;
+    p.n_in = int(e->k);
+    p.width = int64_t(e->L);
+    p.n_obj = 1;
+    return e->ctx->matmul(p);
+}
+
+}  // namespace
+
+extern "C" {
+
+// ------------------------------------------------------------------------------------------------------
+// status text — errors.rs:3-58
+// ------------------------------------------------------------------------------------------------------
+const char *rlnc_status_name(int s) {
+    static const char *names[] = {"Ok",
+                                  "CodingVectorLengthMismatch",
+                                  "DataLengthMismatch",
+                                  "PieceCountZero",
+                                  "DataLengthZero",
+                                  "PieceLengthZero",
+                                  "NotEnoughPiecesToRecode",
+                                  "PieceLengthTooShort",
+                                  "PieceNotUseful",
+                                  "ReceivedAllPieces",
+                                  "NotAllPiecesReceivedYet",
+                                  "InvalidDecodedDataFormat",
+                                  "InvalidPieceLength",
+                                  "InvalidOutputBuffer"};
+    if (s >= 0 && s <= 13) return names[s];
+    switch (s) {
+    case RLNC_ERR_INVALID_ARGUMENT: return "InvalidArgument";
+    case RLNC_ERR_DEVICE: return "DeviceError";
+    case RLNC_ERR_OUT_OF_MEMORY: return "OutOfMemory";
+    case RLNC_ERR_NO_DEVICE: return "NoDevice";
+    default: return "Unknown";
+    }
+}
+
+const char *rlnc_status_message(int s) {
+    static const char *msgs[] = {"Ok",
+                                 "Coding vector length mismatch",
+                                 "Data length mismatch",
+                                 "Piece count is zero",
+                                 "Data length is zero",
+                                 "Piece length is zero",
+                                 "Not enough pieces received to recode",
+                                 "Piece length is too short",
+                                 "Received piece is not useful",
+                                 "Received all pieces",
+                                 "Not all pieces are received yet",
+                                 "Invalid decoded data format",
+                                 "Invalid piece length",
+                                 "Invalid output buffer"};
+    if (s >= 0 && s <= 13) return msgs[s];
+    return rlnc_status_name(s);
+}
+
+const char *rlnc_last_error(void) { return g_last_error.c_str(); }
+const char *rlnc_version(void) { return "rlnc_hip 0.1.0 (gfx950; reference itzmeanjan/rlnc 0.8.5)"; }
+
+// ------------------------------------------------------------------------------------------------------
+// context
+// ------------------------------------------------------------------------------------------------------
+int rlnc_context_create(int device, rlnc_context **out) {
+    CHECK_ARG(out != nullptr);
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return set_error(RLNC_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= count) return set_error(RLNC_ERR_NO_DEVICE, "device %d out of range (%d)", device, count);
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_error(RLNC_ERR_NO_DEVICE, "device %d is %s, librlnc_hip is built for gfx950 only", device,
+                         prop.gcnArchName);
+    auto *c = new (std::nothrow) rlnc_context;
+    if (!c) return set_error(RLNC_ERR_OUT_OF_MEMORY, "context allocation");
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return set_error(RLNC_ERR_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    c->stream = c->own;
+    *out = c;
+    return RLNC_OK;
+}
+
+void rlnc_context_destroy(rlnc_context *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->own) (void)hipStreamDestroy(ctx->own);
+    delete ctx;
+}
+
+int rlnc_context_set_stream(rlnc_context *ctx, void *s) {
+    CHECK_ARG(ctx != nullptr);
+    ctx->stream = s ? static_cast<hipStream_t>(s) : ctx->own;
+    return RLNC_OK;
+}
+
+void *rlnc_context_get_stream(rlnc_context *ctx) { return ctx ? ctx->stream : nullptr; }
+int rlnc_context_device(const rlnc_context *ctx) { return ctx ? ctx->device : -1; }
+
+int rlnc_context_synchronize(rlnc_context *ctx) {
+    CHECK_ARG(ctx != nullptr);
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RLNC_OK;
+}
+
+int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows) {
+    CHECK_ARG(ctx != nullptr);
+    CHECK_ARG(variant == 0 || variant == 1);
+    CHECK_ARG(max_tile_rows == 0 || max_tile_rows == 1 || max_tile_rows == 2 || max_tile_rows == 4 ||
+              max_tile_rows == 8 || max_tile_rows == 16 || max_tile_rows == 32);
+    ctx->variant = static_cast<rlnc::MatmulVariant>(variant);
+    ctx->max_tile_rows = max_tile_rows;
+    return RLNC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------------
+// L1 primitives — simd/mod.rs:18-119 (early-outs on the host, exactly as the reference)
+// ------------------------------------------------------------------------------------------------------
+int rlnc_gf256_inplace_mul_vec_by_scalar(rlnc_context *ctx, uint8_t *vec, size_t len, uint8_t scalar) {
+    CHECK_ARG(ctx != nullptr);
+    if (len == 0) return RLNC_OK;  // :19-21
+    CHECK_ARG(vec != nullptr);
+    int st = ctx->activate();
+    if (st) return st;
+    if (scalar == 0) {  // :22-25
+        HIP_TRY(hipMemsetAsync(vec, 0, len, ctx->stream));
+        return RLNC_OK;
+    }
+    if (scalar == 1) return RLNC_OK;  // :26-28
+    HIP_TRY(rlnc::launch_mul_vec_by_scalar(vec, int64_t(len), scalar, ctx->stream));
+    return RLNC_OK;
+}
+
+int rlnc_gf256_inplace_add_vectors(rlnc_context *ctx, uint8_t *dst, const uint8_t *src, size_t len) {
+    CHECK_ARG(ctx != nullptr);
+    if (len == 0) return RLNC_OK;
+    CHECK_ARG(dst != nullptr && src != nullptr);
+    int st = ctx->activate();
+    if (st) return st;
+    HIP_TRY(rlnc::launch_add_vectors(dst, src, int64_t(len), ctx->stream));
+    return RLNC_OK;
+}
+
+int rlnc_gf256_mul_vec_by_scalar_then_add_into_vec(rlnc_context *ctx, uint8_t *dst, const uint8_t *src, size_t len,
+                                                   uint8_t scalar) {
+    CHECK_ARG(ctx != nullptr);
+    if (len == 0) return RLNC_OK;  // :90-92
+    if (scalar == 0) return RLNC_OK;  // :93-95
+    CHECK_ARG(dst != nullptr && src != nullptr);
+    int st = ctx->activate();
+    if (st) return st;
+    if (scalar == 1) {  // :96-99
+        HIP_TRY(rlnc::launch_add_vectors(dst, src, int64_t(len), ctx->stream));
+        return RLNC_OK;
+    }
+    HIP_TRY(rlnc::launch_mul_add(dst, src, int64_t(len), scalar, ctx->stream));
+    return RLNC_OK;
+}
+
+int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc) {
+    CHECK_ARG(ctx != nullptr && desc != nullptr);
+    CHECK_ARG(desc->n_out >= 0 && desc->n_in >= 0 && desc->width >= 0 && desc->n_obj >= 0);
+    if (desc->n_out == 0 || desc->width == 0 || desc->n_obj == 0) return RLNC_OK;
+    CHECK_ARG(desc->n_in > 0 && desc->in && desc->coef && desc->out);
+    int st = ctx->activate();
+    if (st) return st;
+    rlnc::MatmulParams p;
+    matmul_desc_to_params(desc, p);
+    return ctx->matmul(p);
+}
+
+// ------------------------------------------------------------------------------------------------------
+// Encoder — encoder.rs
+// ------------------------------------------------------------------------------------------------------
+static int encoder_from_host(rlnc_context *ctx, const uint8_t *data, size_t len, size_t k, bool pad, rlnc_encoder **out) {
+    CHECK_ARG(ctx != nullptr && out != nullptr);
+    *out = nullptr;
+    if (len == 0) return RLNC_ERR_DATA_LENGTH_ZERO;  // encoder.rs:86-88 / :51-53
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;    // :89-91 / :54-56
+    CHECK_ARG(data != nullptr);
+    size_t L;
+    if (pad) {
+        L = (len + 1 + k - 1) / k;  // :93-95
+    } else {
+        L = len / k;
+        if (L * k != len) return RLNC_ERR_DATA_LENGTH_MISMATCH;  // :58-64
+    }
+    int st = ctx->activate();
+    if (st) return st;
+    std::unique_ptr<rlnc_encoder> e(new (std::nothrow) rlnc_encoder);
+    if (!e) return set_error(RLNC_ERR_OUT_OF_MEMORY, "encoder allocation");
+    e->ctx = ctx;
+    e->k = k;
+    e->L = L;
+    e->stride = round16(L);
+    e->owned = true;
+    HIP_TRY(hipMalloc(&e->src, k * e->stride));
+    // padded image: data, 0x81 marker, zeros (encoder.rs:98-99), laid out at a 16-B row stride
+    if ((st = ctx->pin_a.ensure(k * e->stride))) return st;
+    uint8_t *h = ctx->pin_a.as<uint8_t>();
+    std::memset(h, 0, k * e->stride);
+    for (size_t r = 0; r < k; ++r) {
+        const size_t off = r * L;
+        if (off < len) std::memcpy(h + r * e->stride, data + off, std::min(L, len - off));
+    }
+    if (pad) h[(len / L) * e->stride + (len % L)] = rlnc::kBoundaryMarker;
+    HIP_TRY(hipMemcpyAsync(e->src, h, k * e->stride, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    *out = e.release();
+    return RLNC_OK;
+}
+
+int rlnc_encoder_new(rlnc_context *ctx, const uint8_t *data, size_t len, size_t k, rlnc_encoder **out) {
+    return encoder_from_host(ctx, data, len, k, true, out);
+}
+
+int rlnc_encoder_without_padding(rlnc_context *ctx, const uint8_t *data, size_t len, size_t k, rlnc_encoder **out) {
+    return encoder_from_host(ctx, data, len, k, false, out);
+}
+
+int rlnc_encoder_from_device(rlnc_context *ctx, const uint8_t *pieces, size_t k, size_t L, size_t row_stride,
+                             rlnc_encoder **out) {
+    CHECK_ARG(ctx != nullptr && out != nullptr);
+    *out = nullptr;
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
+    if (L == 0) return RLNC_ERR_DATA_LENGTH_ZERO;
+    CHECK_ARG(pieces != nullptr && row_stride >= L);
+    auto *e = new (std::nothrow) rlnc_encoder;
+    if (!e) return set_error(RLNC_ERR_OUT_OF_MEMORY, "encoder allocation");
+    e->ctx = ctx;
+    e->k = k;
+    e->L = L;
+    e->stride = row_stride;
+    e->src = const_cast<uint8_t *>(pieces);
+    e->owned = false;
+    *out = e;
+    return RLNC_OK;
+}
+
+void rlnc_encoder_free(rlnc_encoder *e) { delete e; }
+size_t rlnc_encoder_get_piece_count(const rlnc_encoder *e) { return e ? e->k : 0; }
+size_t rlnc_encoder_get_piece_byte_len(const rlnc_encoder *e) { return e ? e->L : 0; }
+size_t rlnc_encoder_get_full_coded_piece_byte_len(const rlnc_encoder *e) { return e ? e->k + e->L : 0; }
+
+int rlnc_encoder_code_with_coding_vector(rlnc_encoder *e, const uint8_t *cv, size_t cv_len, uint8_t *coded,
+                                         size_t coded_len) {
+    CHECK_ARG(e != nullptr);
+    if (cv_len != e->k) return RLNC_ERR_CODING_VECTOR_LENGTH_MISMATCH;  // encoder.rs:129-131
+    if (coded_len != e->L) return RLNC_ERR_INVALID_OUTPUT_BUFFER;       // :132-134
+    CHECK_ARG(cv != nullptr && coded != nullptr);
+    rlnc_context *ctx = e->ctx;
+    int st = ctx->activate();
+    if (st) return st;
+    if ((st = ctx->ws_coef.ensure(e->k)) || (st = ctx->ws_out.ensure(e->L))) return st;
+    HIP_TRY(hipMemcpyAsync(ctx->ws_coef.p, cv, e->k, hipMemcpyHostToDevice, ctx->stream));
+    if ((st = encoder_launch(e, ctx->ws_coef.as<uint8_t>(), int64_t(e->k), 1, ctx->ws_out.as<uint8_t>(),
+                             int64_t(e->L), nullptr, 0)))
+        return st;
+    HIP_TRY(hipMemcpyAsync(coded, ctx->ws_out.p, e->L, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RLNC_OK;
+}
+
+int rlnc_encoder_code_with_buf(rlnc_encoder *e, const uint8_t *rnd, size_t n_rnd, uint8_t *full, size_t full_len) {
+    CHECK_ARG(e != nullptr);
+    if (full_len != e->k + e->L) return RLNC_ERR_INVALID_OUTPUT_BUFFER;  // encoder.rs:242-244
+    if (n_rnd != e->k) return RLNC_ERR_CODING_VECTOR_LENGTH_MISMATCH;    // fill_bytes fills exactly k bytes
+    CHECK_ARG(rnd != nullptr && full != nullptr);
+    std::memmove(full, rnd, e->k);  // :246-248
+    return rlnc_encoder_code_with_coding_vector(e, full, e->k, full + e->k, e->L);
+}
+
+int rlnc_encoder_code_batch_device(rlnc_encoder *e, const uint8_t *coeffs_dev, size_t n, uint8_t *out_dev,
+                                   size_t out_row_stride) {
+    CHECK_ARG(e != nullptr);
+    if (n == 0) return RLNC_OK;
+    CHECK_ARG(coeffs_dev != nullptr && out_dev != nullptr && n <= 0x7FFFFFFF);
+    const size_t row = out_row_stride ? out_row_stride : e->k + e->L;
+    CHECK_ARG(row >= e->k + e->L);
+    int st = e->ctx->activate();
+    if (st) return st;
+    return encoder_launch(e, coeffs_dev, int64_t(e->k), int(n), out_dev + e->k, int64_t(row), out_dev, int64_t(row));
+}
+
+// ------------------------------------------------------------------------------------------------------
+// Recoder — recoder.rs
+// ------------------------------------------------------------------------------------------------------
+int rlnc_recoder_new(rlnc_context *ctx, const uint8_t *data, size_t len, size_t full, size_t k, rlnc_recoder **out) {
+    CHECK_ARG(ctx != nullptr && out != nullptr);
+    *out = nullptr;
+    if (len == 0) return RLNC_ERR_NOT_ENOUGH_PIECES_TO_RECODE;  // recoder.rs:69-71
+    if (full == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;            // :72-74
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;                // :75-77
+    if (full <= k) return RLNC_ERR_PIECE_LENGTH_TOO_SHORT;       // :78-80
+    const size_t n = len / full;                                 // :83 (trailing bytes ignored, :88)
+    if (n == 0) return RLNC_ERR_NOT_ENOUGH_PIECES_TO_RECODE;     // reference: UB (unwrap_unchecked, :97)
+    CHECK_ARG(data != nullptr && n <= 0x7FFFFFFF);
+    int st = ctx->activate();
+    if (st) return st;
+    std::unique_ptr<rlnc_recoder> r(new (std::nothrow) rlnc_recoder);
+    if (!r) return set_error(RLNC_ERR_OUT_OF_MEMORY, "recoder allocation");
+    r->ctx = ctx;
+    r->k = k;
+    r->n = n;
+    r->full = full;
+    r->stride = round16(full);
+    HIP_TRY(hipMalloc(&r->pieces, n * r->stride));
+    HIP_TRY(hipMemcpy2DAsync(r->pieces, r->stride, data, full, full, n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    *out = r.release();
+    return RLNC_OK;
+}
+
+void rlnc_recoder_free(rlnc_recoder *r) { delete r; }
+size_t rlnc_recoder_get_original_num_pieces_coded_together(const rlnc_recoder *r) { return r ? r->k : 0; }
+size_t rlnc_recoder_get_num_pieces_recoded_together(const rlnc_recoder *r) { return r ? r->n : 0; }
+size_t rlnc_recoder_get_piece_byte_len(const rlnc_recoder *r) { return r ? r->full - r->k : 0; }
+size_t rlnc_recoder_get_full_coded_piece_byte_len(const rlnc_recoder *r) { return r ? r->full : 0; }
+
+static int recoder_launch(rlnc_recoder *r, const uint8_t *r_dev, int count, uint8_t *out_dev, int64_t out_row) {
+    // recoded piece = Σ_i r_i · (coeffs_i ‖ data_i): the coefficient fold of recoder.rs:133-144 and the
+    // data combination of :146-150 are the same linear map applied to different columns
+    rlnc::MatmulParams p{};
+    p.in = r->pieces;
+    p.in_row = int64_t(r->stride);
+    p.coef = r_dev;
+    p.coef_row = int64_t(r->n);
+    p.out = out_dev;
+    p.out_row = out_row;
+    p.n_out = count;
+    p.n_in = int(r->n);
+    p.width = int64_t(r->full);
+    p.n_obj = 1;
+    return r->ctx->matmul(p);
+}
+
+int rlnc_recoder_recode_with_buf(rlnc_recoder *r, const uint8_t *rnd, size_t n_rnd, uint8_t *full, size_t full_len) {
+    CHECK_ARG(r != nullptr);
+    if (full_len != r->full) return RLNC_ERR_INVALID_OUTPUT_BUFFER;  // recoder.rs:123-125
+    if (n_rnd != r->n) return RLNC_ERR_CODING_VECTOR_LENGTH_MISMATCH;  // fill_bytes fills exactly n bytes
+    CHECK_ARG(rnd != nullptr && full != nullptr);
+    rlnc_context *ctx = r->ctx;
+    int st = ctx->activate();
+    if (st) return st;
+    if ((st = ctx->ws_coef.ensure(r->n)) || (st = ctx->ws_out.ensure(r->full))) return st;
+    HIP_TRY(hipMemcpyAsync(ctx->ws_coef.p, rnd, r->n, hipMemcpyHostToDevice, ctx->stream));
+    if ((st = recoder_launch(r, ctx->ws_coef.as<uint8_t>(), 1, ctx->ws_out.as<uint8_t>(), int64_t(r->full)))) return st;
+    HIP_TRY(hipMemcpyAsync(full, ctx->ws_out.p, r->full, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RLNC_OK;
+}
+
+int rlnc_recoder_recode_batch_device(rlnc_recoder *r, const uint8_t *r_dev, size_t count, uint8_t *out_dev) {
+    CHECK_ARG(r != nullptr);
+    if (count == 0) return RLNC_OK;
+    CHECK_ARG(r_dev != nullptr && out_dev != nullptr && count <= 0x7FFFFFFF);
+    int st = r->ctx->activate();
+    if (st) return st;
+    return recoder_launch(r, r_dev, int(count), out_dev, int64_t(r->full));
+}
+
+// ------------------------------------------------------------------------------------------------------
+// Decoder — decoder.rs
+// ------------------------------------------------------------------------------------------------------
+int rlnc_decoder_new(rlnc_context *ctx, size_t L, size_t k, rlnc_decoder **out) {
+    CHECK_ARG(ctx != nullptr && out != nullptr);
+    *out = nullptr;
+    if (L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;  // decoder.rs:66-68
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;   // :69-71
+    CHECK_ARG(k <= 0x7FFFFFFF);
+    auto *d = new (std::nothrow) rlnc_decoder;
+    if (!d) return set_error(RLNC_ERR_OUT_OF_MEMORY, "decoder allocation");
+    d->ctx = ctx;
+    d->k = k;
+    d->L = L;
+    d->stride = round16(L);
+    d->elim.reset(new Elimination(k));
+    *out = d;
+    return RLNC_OK;
+}
+
+void rlnc_decoder_free(rlnc_decoder *d) { delete d; }
+
+static int decoder_store_slot(rlnc_decoder *d, int slot, const uint8_t *src, hipMemcpyKind kind) {
+    rlnc_context *ctx = d->ctx;
+    if (size_t(slot) >= d->store_slots) {
+        size_t ns = std::max(d->elim->slots(), size_t(slot) + 1);
+        uint8_t *n = nullptr;
+        HIP_TRY(hipMalloc(&n, ns * d->stride));
+        if (d->store) {
+            HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            (void)hipFree(d->store);
+        }
+        d->store = n;
+        d->store_slots = ns;
+    }
+    HIP_TRY(hipMemcpyAsync(d->store + size_t(slot) * d->stride, src, d->L, kind, ctx->stream));
+    if (kind == hipMemcpyHostToDevice) HIP_TRY(hipStreamSynchronize(ctx->stream));  // caller may reuse the piece
+    return RLNC_OK;
+}
+
+static int decoder_decode_impl(rlnc_decoder *d, const uint8_t *coeffs_host, const uint8_t *data, hipMemcpyKind kind) {
+    int slot = -1;
+    bool keep = false;
+    const int st = d->elim->push(coeffs_host, &slot, &keep);
+    if (st == RLNC_ERR_RECEIVED_ALL_PIECES) return st;
+    d->received += 1;                                     // decoder.rs:107
+    if (st == RLNC_OK) d->useful = d->elim->rank();       // :115
+    if (keep) {
+        int s2 = d->ctx->activate();
+        if (s2) return s2;
+        if ((s2 = decoder_store_slot(d, slot, data, kind))) return s2;
+    }
+    return st;
+}
+
+int rlnc_decoder_decode(rlnc_decoder *d, const uint8_t *piece, size_t len) {
+    CHECK_ARG(d != nullptr);
+    if (d->elim->decoded()) return RLNC_ERR_RECEIVED_ALL_PIECES;  // decoder.rs:97-99
+    if (len != d->k + d->L) return RLNC_ERR_INVALID_PIECE_LENGTH; // :100-102
+    CHECK_ARG(piece != nullptr);
+    return decoder_decode_impl(d, piece, piece + d->k, hipMemcpyHostToDevice);
+}
+
+int rlnc_decoder_decode_device(rlnc_decoder *d, const uint8_t *piece_dev, size_t len) {
+    CHECK_ARG(d != nullptr);
+    if (d->elim->decoded()) return RLNC_ERR_RECEIVED_ALL_PIECES;
+    if (len != d->k + d->L) return RLNC_ERR_INVALID_PIECE_LENGTH;
+    CHECK_ARG(piece_dev != nullptr);
+    rlnc_context *ctx = d->ctx;
+    int st = ctx->activate();
+    if (st) return st;
+    if ((st = ctx->pin_c.ensure(d->k))) return st;
+    HIP_TRY(hipMemcpyAsync(ctx->pin_c.p, piece_dev, d->k, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    std::vector<uint8_t> coeffs(ctx->pin_c.as<uint8_t>(), ctx->pin_c.as<uint8_t>() + d->k);
+    return decoder_decode_impl(d, coeffs.data(), piece_dev + d->k, hipMemcpyDeviceToDevice);
+}
+
+int rlnc_decoder_is_already_decoded(const rlnc_decoder *d) { return d && d->elim->decoded() ? 1 : 0; }
+size_t rlnc_decoder_get_num_pieces_coded_together(const rlnc_decoder *d) { return d ? d->k : 0; }
+size_t rlnc_decoder_get_piece_byte_len(const rlnc_decoder *d) { return d ? d->L : 0; }
+size_t rlnc_decoder_get_full_coded_piece_byte_len(const rlnc_decoder *d) { return d ? d->k + d->L : 0; }
+size_t rlnc_decoder_get_received_piece_count(const rlnc_decoder *d) { return d ? d->received : 0; }
+size_t rlnc_decoder_get_useful_piece_count(const rlnc_decoder *d) { return d ? d->useful : 0; }
+size_t rlnc_decoder_get_remaining_piece_count(const rlnc_decoder *d) { return d ? d->k - d->useful : 0; }
+
+// decoded rows = T × stored data rows, written to out_dev [k][L]
+static int decoder_apply(rlnc_decoder *d, uint8_t *out_dev) {
+    rlnc_context *ctx = d->ctx;
+    const size_t slots = d->elim->slots();
+    int st;
+    if ((st = ctx->pin_b.ensure(d->k * slots)) || (st = ctx->ws_coef.ensure(d->k * slots))) return st;
+    d->elim->transform(ctx->pin_b.as<uint8_t>(), slots);
+    HIP_TRY(hipMemcpyAsync(ctx->ws_coef.p, ctx->pin_b.p, d->k * slots, hipMemcpyHostToDevice, ctx->stream));
+    if (d->store_slots < slots) {
+        // slots never stored were never referenced; give them zero rows so T × D is well defined
+        uint8_t *n = nullptr;
+        HIP_TRY(hipMalloc(&n, slots * d->stride));
+        HIP_TRY(hipMemsetAsync(n, 0, slots * d->stride, ctx->stream));
+        if (d->store)
+            HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        if (d->store) (void)hipFree(d->store);
+        d->store = n;
+        d->store_slots = slots;
+    }
+    rlnc::MatmulParams p{};
+    p.in = d->store;
+    p.in_row = int64_t(d->stride);
+    p.coef = ctx->ws_coef.as<uint8_t>();
+    p.coef_row = int64_t(slots);
+    p.out = out_dev;
+    p.out_row = int64_t(d->L);
+    p.n_out = int(d->k);
+    p.n_in = int(slots);
+    p.width = int64_t(d->L);
+    p.n_obj = 1;
+    return ctx->matmul(p);
+}
+
+int rlnc_decoder_get_decoded_data(rlnc_decoder *d, uint8_t *out, size_t cap, size_t *out_len) {
+    CHECK_ARG(d != nullptr);
+    if (!d->elim->decoded()) return RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;  // decoder.rs:137-139
+    CHECK_ARG(out != nullptr && out_len != nullptr && cap >= d->k * d->L);
+    rlnc_context *ctx = d->ctx;
+    int st = ctx->activate();
+    if (st) return st;
+    if ((st = ctx->ws_out.ensure(d->k * d->L))) return st;
+    if ((st = decoder_apply(d, ctx->ws_out.as<uint8_t>()))) return st;
+    HIP_TRY(hipMemcpyAsync(out, ctx->ws_out.p, d->k * d->L, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    // get_final_data_len — decoder.rs:162-177: last nonzero byte must be the 0x81 marker, not at 0
+    size_t n = d->k * d->L;
+    while (n > 0 && out[n - 1] == 0) --n;
+    if (n == 0 || out[n - 1] != rlnc::kBoundaryMarker || n - 1 == 0) return RLNC_ERR_INVALID_DECODED_DATA_FORMAT;
+    *out_len = n - 1;
+    return RLNC_OK;
+}
+
+int rlnc_decoder_get_decoded_data_device(rlnc_decoder *d, uint8_t *out_dev, size_t cap, size_t *out_len) {
+    CHECK_ARG(d != nullptr);
+    if (!d->elim->decoded()) return RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;
+    CHECK_ARG(out_dev != nullptr && out_len != nullptr && cap >= d->k * d->L);
+    rlnc_context *ctx = d->ctx;
+    int st = ctx->activate();
+    if (st) return st;
+    if ((st = decoder_apply(d, out_dev))) return st;
+    if ((st = ctx->ws_scan.ensure(8)) || (st = ctx->ws_status.ensure(4)) || (st = ctx->ws_len.ensure(8)) ||
+        (st = ctx->pin_c.ensure(16)))
+        return st;
+    HIP_TRY(rlnc::launch_final_data_len(out_dev, 0, int64_t(d->k * d->L), 1, ctx->ws_scan.as<unsigned long long>(),
+                                        ctx->ws_status.as<int32_t>(), ctx->ws_len.as<int64_t>(),
+                                        RLNC_ERR_INVALID_DECODED_DATA_FORMAT, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->pin_c.p, ctx->ws_status.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->pin_c.as<uint8_t>() + 8, ctx->ws_len.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    const int32_t status = *ctx->pin_c.as<int32_t>();
+    if (status) return status;
+    std::memcpy(out_len, ctx->pin_c.as<uint8_t>() + 8, 8);
+    return RLNC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------------
+// batch API
+// ------------------------------------------------------------------------------------------------------
+int rlnc_encode_batch(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t nobj, const uint8_t *coeffs,
+                      size_t n, uint8_t *pieces) {
+    CHECK_ARG(ctx != nullptr);
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
+    if (L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;
+    if (n == 0 || nobj == 0) return RLNC_OK;
+    CHECK_ARG(src && coeffs && pieces && n <= 0x7FFFFFFF && k <= 0x7FFFFFFF && nobj <= 0x7FFFFFFF);
+    int st = ctx->activate();
+    if (st) return st;
+    const int64_t full = int64_t(k + L);
+    rlnc::MatmulParams p{};
+    p.in = src;
+    p.in_obj = int64_t(k * L);
+    p.in_row = int64_t(L);
+    p.coef = coeffs;
+    p.coef_obj = int64_t(n * k);
+    p.coef_row = int64_t(k);
+    p.out = pieces + k;
+    p.out_obj = int64_t(n) * full;
+    p.out_row = full;
+    p.hdr = pieces;
+    p.hdr_obj = int64_t(n) * full;
+    p.hdr_row = full;
+    p.n_out = int(n);
+    p.n_in = int(k);
+    p.width = int64_t(L);
+    p.n_obj = int(nobj);
+    return ctx->matmul(p);
+}
+
+int rlnc_recode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t k, size_t L, size_t n, size_t nobj,
+                      const uint8_t *r, size_t count, uint8_t *out) {
+    CHECK_ARG(ctx != nullptr);
+    if (n == 0) return RLNC_ERR_NOT_ENOUGH_PIECES_TO_RECODE;
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
+    if (L == 0) return RLNC_ERR_PIECE_LENGTH_TOO_SHORT;
+    if (count == 0 || nobj == 0) return RLNC_OK;
+    CHECK_ARG(pieces && r && out && n <= 0x7FFFFFFF && count <= 0x7FFFFFFF && nobj <= 0x7FFFFFFF);
+    int st = ctx->activate();
+    if (st) return st;
+    const int64_t full = int64_t(k + L);
+    rlnc::MatmulParams p{};
+    p.in = pieces;
+    p.in_obj = int64_t(n) * full;
+    p.in_row = full;
+    p.coef = r;
+    p.coef_obj = int64_t(count * n);
+    p.coef_row = int64_t(n);
+    p.out = out;
+    p.out_obj = int64_t(count) * full;
+    p.out_row = full;
+    p.n_out = int(count);
+    p.n_in = int(n);
+    p.width = full;
+    p.n_obj = int(nobj);
+    return ctx->matmul(p);
+}
+
+int rlnc_decode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L, size_t m,
+                      size_t nobj, uint8_t *decoded, int32_t *piece_status, int32_t *object_status,
+                      uint64_t *data_len) {
+    CHECK_ARG(ctx != nullptr);
+    if (L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
+    if (nobj == 0) return RLNC_OK;
+    CHECK_ARG(pieces && decoded && m > 0 && m <= 0x7FFFFFFF && k <= 0x7FFFFFFF && nobj <= 0x7FFFFFFF);
+    int st = ctx->activate();
+    if (st) return st;
+    const size_t full = k + L;
+    if (obj_stride == 0) obj_stride = m * full;
+    CHECK_ARG(obj_stride >= m * full);
+    // 1. coefficient headers → host (k bytes of each piece)
+    if ((st = ctx->pin_a.ensure(nobj * m * k))) return st;
+    uint8_t *hdr = ctx->pin_a.as<uint8_t>();
+    if (obj_stride == m * full) {
+        HIP_TRY(hipMemcpy2DAsync(hdr, k, pieces, full, k, nobj * m, hipMemcpyDeviceToHost, ctx->stream));
+    } else {
+        for (size_t o = 0; o < nobj; ++o)
+            HIP_TRY(hipMemcpy2DAsync(hdr + o * m * k, k, pieces + o * obj_stride, full, k, m, hipMemcpyDeviceToHost,
+                                     ctx->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    // 2. exact incremental elimination per object (decoder.rs:96-118 for pieces 0..m-1), host threads
+    if ((st = ctx->pin_b.ensure(nobj * k * m))) return st;
+    uint8_t *T = ctx->pin_b.as<uint8_t>();
+    std::vector<int32_t> ranks(nobj, 0);
+    std::vector<int32_t> pst(nobj * m, 0);
+    auto work = [&](size_t o0, size_t o1) {
+        for (size_t o = o0; o < o1; ++o) {
+            Elimination e(k, m);
+            for (size_t p = 0; p < m; ++p) {
+                int slot;
+                bool keep;
+                pst[o * m + p] = e.push(hdr + (o * m + p) * k, &slot, &keep);
+            }
+            ranks[o] = int32_t(e.rank());
+            std::memset(T + o * k * m, 0, k * m);
+            e.transform(T + o * k * m, m);
+        }
+    };
+    const size_t hw = std::max<unsigned>(1, std::thread::hardware_concurrency());
+    const size_t nth = std::min<size_t>({nobj, hw, 16});
+    if (nth <= 1) {
+        work(0, nobj);
+    } else {
+        std::vector<std::thread> th;
+        const size_t per = (nobj + nth - 1) / nth;
+        for (size_t t = 0; t < nth; ++t) {
+            const size_t a = t * per, b = std::min(nobj, a + per);
+            if (a < b) th.emplace_back(work, a, b);
+        }
+        for (auto &t : th) t.join();
+    }
+    // 3. T → device, decoded = T × received data rows (one launch for all objects)
+    if ((st = ctx->ws_coef.ensure(nobj * k * m))) return st;
+    HIP_TRY(hipMemcpyAsync(ctx->ws_coef.p, T, nobj * k * m, hipMemcpyHostToDevice, ctx->stream));
+    rlnc::MatmulParams p{};
+    p.in = pieces + k;
+    p.in_obj = int64_t(obj_stride);
+    p.in_row = int64_t(full);
+    p.coef = ctx->ws_coef.as<uint8_t>();
+    p.coef_obj = int64_t(k * m);
+    p.coef_row = int64_t(m);
+    p.out = decoded;
+    p.out_obj = int64_t(k * L);
+    p.out_row = int64_t(L);
+    p.n_out = int(k);
+    p.n_in = int(m);
+    p.width = int64_t(L);
+    p.n_obj = int(nobj);
+    if ((st = ctx->matmul(p))) return st;
+    // 4. get_final_data_len on device (decoder.rs:162-177)
+    if ((st = ctx->ws_scan.ensure(nobj * 8)) || (st = ctx->ws_status.ensure(nobj * 4)) ||
+        (st = ctx->ws_len.ensure(nobj * 8)) || (st = ctx->pin_c.ensure(nobj * 16)))
+        return st;
+    HIP_TRY(rlnc::launch_final_data_len(decoded, int64_t(k * L), int64_t(k * L), int(nobj),
+                                        ctx->ws_scan.as<unsigned long long>(), ctx->ws_status.as<int32_t>(),
+                                        ctx->ws_len.as<int64_t>(), RLNC_ERR_INVALID_DECODED_DATA_FORMAT, ctx->stream));
+    int32_t *hst = ctx->pin_c.as<int32_t>();
+    int64_t *hlen = reinterpret_cast<int64_t *>(ctx->pin_c.as<uint8_t>() + nobj * 8);
+    HIP_TRY(hipMemcpyAsync(hst, ctx->ws_status.p, nobj * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(hlen, ctx->ws_len.p, nobj * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (size_t o = 0; o < nobj; ++o) {
+        const bool done = size_t(ranks[o]) == k;
+        if (object_status) object_status[o] = done ? hst[o] : RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;
+        if (data_len) data_len[o] = (done && hst[o] == 0) ? uint64_t(hlen[o]) : 0;
+    }
+    if (piece_status) std::memcpy(piece_status, pst.data(), nobj * m * sizeof(int32_t));
+    return RLNC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------------
+// host-only access to the decoder's elimination engine (no device needed; CPU-testable host logic)
+// ------------------------------------------------------------------------------------------------------
+struct rlnc_elimination {
+    Elimination e;
+    explicit rlnc_elimination(size_t k, size_t fixed) : e(k, fixed) {}
+};
+
+int rlnc_elimination_new(size_t k, size_t fixed_slots, rlnc_elimination **out) {
+    CHECK_ARG(out != nullptr);
+    *out = nullptr;
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
+    *out = new (std::nothrow) rlnc_elimination(k, fixed_slots);
+    return *out ? RLNC_OK : set_error(RLNC_ERR_OUT_OF_MEMORY, "elimination allocation");
+}
+void rlnc_elimination_free(rlnc_elimination *e) { delete e; }
+int rlnc_elimination_push(rlnc_elimination *e, const uint8_t *coeffs, int32_t *slot, int32_t *keep) {
+    CHECK_ARG(e != nullptr && coeffs != nullptr);
+    int s = -1;
+    bool k = false;
+    const int st = e->e.push(coeffs, &s, &k);
+    if (slot) *slot = s;
+    if (keep) *keep = k ? 1 : 0;
+    return st;
+}
+size_t rlnc_elimination_rank(const rlnc_elimination *e) { return e ? e->e.rank() : 0; }
+size_t rlnc_elimination_slots(const rlnc_elimination *e) { return e ? e->e.slots() : 0; }
+int rlnc_elimination_transform(const rlnc_elimination *e, uint8_t *T, size_t ld) {
+    CHECK_ARG(e != nullptr && T != nullptr && ld >= e->e.slots());
+    std::memset(T, 0, e->e.k() * ld);
+    e->e.transform(T, ld);
+    return RLNC_OK;
+}
+int rlnc_elimination_coefficients(const rlnc_elimination *e, uint8_t *C) {
+    CHECK_ARG(e != nullptr && C != nullptr);
+    for (size_t r = 0; r < e->e.rank(); ++r) std::memcpy(C + r * e->e.k(), e->e.row(r), e->e.k());
+    return RLNC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,386 @@
+// kernels.hip — hand-written gfx950 (CDNA4) kernels for the RLNC GF(2^8) hot path.
+//
+// The reference's one hot primitive is dst ^= c·src over GF(2^8) (src/common/simd/mod.rs:89-119), called
+// k times per coded piece by the encoder (encoder.rs:138-141), n times per recoded piece
+// (recoder.rs:146-150) and ≈k² times per object by the decoder's RREF (decoder_matrix.rs:143-211).
+// On MI355X that call is far too small to launch (1 MiB ≈ 0.13 µs of HBM time), so the device operator
+// is the matrix form Out = Coef ⊗ In (kernels.hpp) with one workgroup per 4 KiB column block × row tile.
+//
+// GF multiply on CDNA4 without MFMA (byte-field arithmetic, not a dense FP contraction):
+//   c·x = T0[x & 7] ^ T1[(x >> 3) & 7] ^ T2[x >> 6]      (3-bit split; T0/T1 8 entries, T2 4 entries)
+// Each table fits in two VGPR dwords, and v_perm_b32 looks up FOUR bytes per instruction (one per byte
+// lane of the selector), so one multiply-accumulate of a 32-bit word costs 3 v_perm_b32 + 1.5 v_bitop3_b32
+// (3-way XOR).  The per-coefficient tables are built once per workgroup into LDS and read back as
+// broadcast ds_read_b128/b32 (every lane reads the same address).  The selectors depend only on the
+// source word, so they are computed once per source row and reused by all NT output rows of the tile.
+//
+// A second variant (NibbleLds) keeps the reference's 4-bit split tables (simd_mul_table.rs:36-80,
+// LOW[c][x&15] ^ HIGH[c][x>>4]) in LDS and looks them up one byte per lane per ds_read_u8, i.e. the
+// north-star's literal design; it is kept as the ablation baseline.
+#include <hip/hip_runtime.h>
+
+#include "gf256.hpp"
+#include "kernels.hpp"
+
+namespace rlnc {
+
+namespace {
+
+constexpr int kThreads = 256;          // 4 waves
+constexpr int kBytesPerThread = 16;    // one dwordx4 per source row per lane
+constexpr int kColBlock = kThreads * kBytesPerThread;  // 4 KiB of columns per workgroup
+constexpr int kKC = 32;                // coefficient chunk (tables per chunk staged in LDS)
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+template <bool ALIGNED>
+__device__ __forceinline__ uint4 load16(const uint8_t *p, int nbytes) {
+    if (ALIGNED && nbytes == 16) return *reinterpret_cast<const uint4 *>(p);
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        if (b < nbytes) w[b >> 2] |= uint32_t(p[b]) << (8 * (b & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <bool ALIGNED>
+__device__ __forceinline__ void store16(uint8_t *p, uint4 v, int nbytes) {
+    if (ALIGNED && nbytes == 16) {
+        *reinterpret_cast<uint4 *>(p) = v;
+        return;
+    }
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        if (b < nbytes) p[b] = uint8_t(w[b >> 2] >> (8 * (b & 3)));
+}
+
+struct Sel {
+    uint32_t s0[4], s1[4], s2[4];
+};
+
+__device__ __forceinline__ Sel selectors(uint4 x) {
+    Sel s;
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        s.s0[q] = w[q] & 0x07070707u;
+        s.s1[q] = (w[q] >> 3) & 0x07070707u;
+        s.s2[q] = (w[q] >> 6) & 0x03030303u;
+    }
+    return s;
+}
+
+// XCD-aware work decode (cdna_hip_programming.md §5.5 T1): blocks b and b+8 share an XCD, so give every
+// XCD a contiguous range of work items, ordered row-tile-fastest: the row tiles of one column block then
+// run on one XCD and re-read that block's source rows from its L2 instead of HBM.
+__device__ __forceinline__ void decode_block(int total, int row_tiles, int col_blocks, int &rt, int &cb, int &obj) {
+    int b = blockIdx.x;
+    int w = b;
+    if ((total & 7) == 0) {
+        const int per = total >> 3;
+        w = (b & 7) * per + (b >> 3);
+    }
+    rt = w % row_tiles;
+    const int rest = w / row_tiles;
+    cb = rest % col_blocks;
+    obj = rest / col_blocks;
+}
+
+template <int NT, bool ALIGNED>
+__global__ __launch_bounds__(kThreads) void gf_matmul_perm_kernel(MatmulParams p, int row_tiles, int col_blocks) {
+    __shared__ uint4 s_t01[kKC][NT];
+    __shared__ uint32_t s_t2[kKC][NT];
+
+    int rt, cb, obj;
+    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    const int row0 = rt * NT;
+    const int rows_here = min(NT, p.n_out - row0);
+    const int64_t col = int64_t(cb) * kColBlock + int64_t(threadIdx.x) * kBytesPerThread;
+    const int nbytes = col < p.width ? int(min<int64_t>(kBytesPerThread, p.width - col)) : 0;
+    const uint8_t *in_base = p.in + int64_t(obj) * p.in_obj + col;
+    const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
+
+    uint32_t acc[NT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0u;
+
+    for (int j0 = 0; j0 < p.n_in; j0 += kKC) {
+        const int kc = min(kKC, p.n_in - j0);
+        if (j0) __syncthreads();  // the previous chunk's tables are consumed
+        for (int e = threadIdx.x; e < kKC * NT; e += kThreads) {
+            const int i = e % NT, j = e / NT;
+            const uint8_t c = (i < rows_here && j < kc) ? coef_base[int64_t(i) * p.coef_row + j0 + j] : uint8_t(0);
+            const PermTable t = make_perm_table(c);
+            s_t01[j][i] = make_uint4(t.t0lo, t.t0hi, t.t1lo, t.t1hi);
+            s_t2[j][i] = t.t2;
+        }
+        __syncthreads();
+        if (nbytes > 0) {
+            const uint8_t *rowp = in_base + int64_t(j0) * p.in_row;
+            uint4 na = load16<ALIGNED>(rowp, nbytes);
+            uint4 nb = kc > 1 ? load16<ALIGNED>(rowp + p.in_row, nbytes) : make_uint4(0, 0, 0, 0);
+            for (int j = 0; j < kc; j += 2) {
+                const uint4 xa = na, xb = nb;
+                // software prefetch of the next row pair while this pair is multiplied
+                if (j + 2 < kc) na = load16<ALIGNED>(rowp + int64_t(j + 2) * p.in_row, nbytes);
+                nb = (j + 3 < kc) ? load16<ALIGNED>(rowp + int64_t(j + 3) * p.in_row, nbytes) : make_uint4(0, 0, 0, 0);
+                const Sel a = selectors(xa);
+                const Sel b = selectors(xb);
+#pragma unroll
+                for (int i = 0; i < NT; ++i) {
+                    const uint4 ta = s_t01[j][i];
+                    const uint32_t ta2 = s_t2[j][i];
+                    const uint4 tb = s_t01[j + 1][i];  // zero table when j+1 == kc
+                    const uint32_t tb2 = s_t2[j + 1][i];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        uint32_t r = xor3(acc[i][q], vperm(ta.y, ta.x, a.s0[q]), vperm(ta.w, ta.z, a.s1[q]));
+                        r = xor3(r, vperm(ta2, ta2, a.s2[q]), vperm(tb.y, tb.x, b.s0[q]));
+                        acc[i][q] = xor3(r, vperm(tb.w, tb.z, b.s1[q]), vperm(tb2, tb2, b.s2[q]));
+                    }
+                }
+            }
+        }
+    }
+
+    if (nbytes > 0) {
+        uint8_t *out_base = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + col;
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+            if (i < rows_here)
+                store16<ALIGNED>(out_base + int64_t(i) * p.out_row,
+                                 make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]), nbytes);
+    }
+    if (p.hdr != nullptr && cb == 0) {
+        uint8_t *h = p.hdr + int64_t(obj) * p.hdr_obj + int64_t(row0) * p.hdr_row;
+        for (int e = threadIdx.x; e < rows_here * p.n_in; e += kThreads) {
+            const int i = e / p.n_in, j = e % p.n_in;
+            h[int64_t(i) * p.hdr_row + j] = coef_base[int64_t(i) * p.coef_row + j];
+        }
+    }
+}
+
+// Ablation baseline: the reference's 4-bit split (LOW/HIGH nibble tables, simd_mul_table.rs:36-80) in
+// LDS, one ds_read_u8 per nibble per byte per lane.
+template <int NT, bool ALIGNED>
+__global__ __launch_bounds__(kThreads) void gf_matmul_nibble_kernel(MatmulParams p, int row_tiles, int col_blocks) {
+    __shared__ uint8_t s_tab[kKC][NT][32];  // [0:16) LOW[c][i]=c·i, [16:32) HIGH[c][i]=c·(i<<4)
+
+    int rt, cb, obj;
+    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    const int row0 = rt * NT;
+    const int rows_here = min(NT, p.n_out - row0);
+    const int64_t col = int64_t(cb) * kColBlock + int64_t(threadIdx.x) * kBytesPerThread;
+    const int nbytes = col < p.width ? int(min<int64_t>(kBytesPerThread, p.width - col)) : 0;
+    const uint8_t *in_base = p.in + int64_t(obj) * p.in_obj + col;
+    const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
+
+    uint32_t acc[NT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0u;
+
+    for (int j0 = 0; j0 < p.n_in; j0 += kKC) {
+        const int kc = min(kKC, p.n_in - j0);
+        if (j0) __syncthreads();
+        for (int e = threadIdx.x; e < kKC * NT * 16; e += kThreads) {
+            const int v = e & 15, i = (e >> 4) % NT, j = (e >> 4) / NT;
+            const uint8_t c = (i < rows_here && j < kc) ? coef_base[int64_t(i) * p.coef_row + j0 + j] : uint8_t(0);
+            s_tab[j][i][v] = gf_mul_slow(c, uint8_t(v));
+            s_tab[j][i][16 + v] = gf_mul_slow(c, uint8_t(v << 4));
+        }
+        __syncthreads();
+        if (nbytes > 0) {
+            for (int j = 0; j < kc; ++j) {
+                const uint4 x = load16<ALIGNED>(in_base + int64_t(j0 + j) * p.in_row, nbytes);
+                const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int i = 0; i < NT; ++i) {
+                    const uint8_t *t = s_tab[j][i];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        uint32_t r = 0;
+#pragma unroll
+                        for (int bb = 0; bb < 4; ++bb) {
+                            const uint32_t byte = (w[q] >> (8 * bb)) & 0xFFu;
+                            r |= uint32_t(t[byte & 15] ^ t[16 + (byte >> 4)]) << (8 * bb);
+                        }
+                        acc[i][q] ^= r;
+                    }
+                }
+            }
+        }
+    }
+    if (nbytes > 0) {
+        uint8_t *out_base = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + col;
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+            if (i < rows_here)
+                store16<ALIGNED>(out_base + int64_t(i) * p.out_row,
+                                 make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]), nbytes);
+    }
+    if (p.hdr != nullptr && cb == 0) {
+        uint8_t *h = p.hdr + int64_t(obj) * p.hdr_obj + int64_t(row0) * p.hdr_row;
+        for (int e = threadIdx.x; e < rows_here * p.n_in; e += kThreads) {
+            const int i = e / p.n_in, j = e % p.n_in;
+            h[int64_t(i) * p.hdr_row + j] = coef_base[int64_t(i) * p.coef_row + j];
+        }
+    }
+}
+
+template <int NT>
+hipError_t launch_nt(const MatmulParams &p, hipStream_t s, MatmulVariant v, bool aligned) {
+    const int row_tiles = (p.n_out + NT - 1) / NT;
+    const int col_blocks = int((p.width + kColBlock - 1) / kColBlock);
+    const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
+    if (total <= 0) return hipSuccess;
+    if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    const dim3 grid{unsigned(total)}, block{unsigned(kThreads)};
+    if (v == MatmulVariant::NibbleLds) {
+        if (aligned)
+            hipLaunchKernelGGL((gf_matmul_nibble_kernel<NT, true>), grid, block, 0, s, p, row_tiles, col_blocks);
+        else
+            hipLaunchKernelGGL((gf_matmul_nibble_kernel<NT, false>), grid, block, 0, s, p, row_tiles, col_blocks);
+    } else {
+        if (aligned)
+            hipLaunchKernelGGL((gf_matmul_perm_kernel<NT, true>), grid, block, 0, s, p, row_tiles, col_blocks);
+        else
+            hipLaunchKernelGGL((gf_matmul_perm_kernel<NT, false>), grid, block, 0, s, p, row_tiles, col_blocks);
+    }
+    return hipGetLastError();
+}
+
+inline bool al16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
+inline bool al16(int64_t v) { return (v & 15) == 0; }
+
+// ---------------------------------------------------------------------------------------------------
+// element-wise primitives (simd/mod.rs:18-119); the scalar early-outs are taken on the host
+// ---------------------------------------------------------------------------------------------------
+template <int OP, bool ALIGNED>  // OP 0: v = c·v   1: d ^= s   2: d ^= c·s
+__global__ __launch_bounds__(kThreads) void gf_vec_kernel(uint8_t *dst, const uint8_t *src, int64_t len, uint32_t t0lo,
+                                                          uint32_t t0hi, uint32_t t1lo, uint32_t t1hi, uint32_t t2) {
+    const int64_t stride = int64_t(gridDim.x) * kThreads * kBytesPerThread;
+    for (int64_t off = (int64_t(blockIdx.x) * kThreads + threadIdx.x) * kBytesPerThread; off < len; off += stride) {
+        const int nb = int(min<int64_t>(kBytesPerThread, len - off));
+        const uint4 x = load16<ALIGNED>((OP == 0 ? dst : src) + off, nb);
+        uint4 r;
+        if (OP == 1) {
+            r = x;
+        } else {
+            const Sel s = selectors(x);
+            uint32_t o[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = xor3(vperm(t0hi, t0lo, s.s0[q]), vperm(t1hi, t1lo, s.s1[q]), vperm(t2, t2, s.s2[q]));
+            r = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+        if (OP != 0) {
+            const uint4 d = load16<ALIGNED>(dst + off, nb);
+            r = make_uint4(r.x ^ d.x, r.y ^ d.y, r.z ^ d.z, r.w ^ d.w);
+        }
+        store16<ALIGNED>(dst + off, r, nb);
+    }
+}
+
+template <int OP>
+hipError_t launch_vec(uint8_t *dst, const uint8_t *src, int64_t len, uint8_t c, hipStream_t s) {
+    if (len <= 0) return hipSuccess;
+    const PermTable t = make_perm_table(c);
+    const int64_t chunks = (len + kBytesPerThread - 1) / kBytesPerThread;
+    const int blocks = int(std::min<int64_t>((chunks + kThreads - 1) / kThreads, 2048));
+    const bool aligned = al16(dst) && (OP == 0 || al16(src));
+    if (aligned)
+        hipLaunchKernelGGL((gf_vec_kernel<OP, true>), dim3(blocks), dim3(kThreads), 0, s, dst, src, len, t.t0lo, t.t0hi,
+                           t.t1lo, t.t1hi, t.t2);
+    else
+        hipLaunchKernelGGL((gf_vec_kernel<OP, false>), dim3(blocks), dim3(kThreads), 0, s, dst, src, len, t.t0lo, t.t0hi,
+                           t.t1lo, t.t1hi, t.t2);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------------
+// get_final_data_len on device (decoder.rs:162-177).  Equivalent formulation: the last nonzero byte of
+// the padded payload must be the boundary marker and must not sit at index 0.
+// ---------------------------------------------------------------------------------------------------
+template <bool ALIGNED>
+__global__ __launch_bounds__(kThreads) void last_nonzero_kernel(const uint8_t *data, int64_t obj_stride, int64_t len,
+                                                                unsigned long long *best) {
+    const int obj = blockIdx.y;
+    const uint8_t *d = data + int64_t(obj) * obj_stride;
+    unsigned long long mine = 0;  // index + 1 of the last nonzero byte seen, 0 = none
+    const int64_t stride = int64_t(gridDim.x) * kThreads * kBytesPerThread;
+    for (int64_t off = (int64_t(blockIdx.x) * kThreads + threadIdx.x) * kBytesPerThread; off < len; off += stride) {
+        const int nb = int(min<int64_t>(kBytesPerThread, len - off));
+        const uint4 x = load16<ALIGNED>(d + off, nb);
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (w[q]) mine = (unsigned long long)(off + 4 * q + (31 - __builtin_clz(w[q])) / 8 + 1);
+    }
+    // wave reduce then one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(mine, off);
+        mine = o > mine ? o : mine;
+    }
+    if ((threadIdx.x & 63) == 0 && mine) atomicMax(best + obj, mine);
+}
+
+__global__ void final_len_kernel(const uint8_t *data, int64_t obj_stride, int n_obj, const unsigned long long *best,
+                                 int32_t *status, int64_t *final_len, int32_t invalid_code) {
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= n_obj) return;
+    const unsigned long long b = best[o];
+    const int64_t idx = int64_t(b) - 1;
+    const bool ok = b != 0 && idx != 0 && data[int64_t(o) * obj_stride + idx] == kBoundaryMarker;
+    status[o] = ok ? 0 : invalid_code;
+    final_len[o] = ok ? idx : 0;
+}
+
+}  // namespace
+
+hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v) {
+    if (p.n_out <= 0 || p.width <= 0 || p.n_obj <= 0) return hipSuccess;
+    const bool aligned = al16(p.in) && al16(p.out) && al16(p.in_row) && al16(p.out_row) &&
+                         (p.n_obj == 1 || (al16(p.in_obj) && al16(p.out_obj)));
+    if (p.n_in <= 0) return hipErrorInvalidValue;
+    if (p.n_out <= 1) return launch_nt<1>(p, s, v, aligned);
+    if (p.n_out <= 2) return launch_nt<2>(p, s, v, aligned);
+    if (p.n_out <= 4) return launch_nt<4>(p, s, v, aligned);
+    if (p.n_out <= 8) return launch_nt<8>(p, s, v, aligned);
+    if (p.n_out <= 16) return launch_nt<16>(p, s, v, aligned);
+    return launch_nt<32>(p, s, v, aligned);
+}
+
+hipError_t launch_mul_vec_by_scalar(uint8_t *vec, int64_t len, uint8_t scalar, hipStream_t s) {
+    return launch_vec<0>(vec, nullptr, len, scalar, s);
+}
+hipError_t launch_add_vectors(uint8_t *dst, const uint8_t *src, int64_t len, hipStream_t s) {
+    return launch_vec<1>(dst, src, len, 1, s);
+}
+hipError_t launch_mul_add(uint8_t *dst, const uint8_t *src, int64_t len, uint8_t scalar, hipStream_t s) {
+    return launch_vec<2>(dst, src, len, scalar, s);
+}
+
+hipError_t launch_final_data_len(const uint8_t *data, int64_t obj_stride, int64_t len, int n_obj,
+                                 unsigned long long *scratch, int32_t *status, int64_t *final_len,
+                                 int32_t invalid_code, hipStream_t s) {
+    if (n_obj <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(scratch, 0, sizeof(unsigned long long) * n_obj, s);
+    if (e != hipSuccess) return e;
+    const int64_t chunks = (len + kBytesPerThread - 1) / kBytesPerThread;
+    const int bx = int(std::min<int64_t>(std::max<int64_t>((chunks + kThreads - 1) / kThreads / 4, 1), 1024));
+    if (al16(data) && (n_obj == 1 || al16(obj_stride)))
+        hipLaunchKernelGGL(last_nonzero_kernel<true>, dim3(bx, n_obj), dim3(kThreads), 0, s, data, obj_stride, len, scratch);
+    else
+        hipLaunchKernelGGL(last_nonzero_kernel<false>, dim3(bx, n_obj), dim3(kThreads), 0, s, data, obj_stride, len, scratch);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(final_len_kernel, dim3((n_obj + 255) / 256), dim3(256), 0, s, data, obj_stride, n_obj, scratch,
+                       status, final_len, invalid_code);
+    return hipGetLastError();
+}
+
+}  // namespace rlnc

@@ -1,0 +1,365 @@
+"""GPU parity: librlnc_hip (through the C ABI) against the oracle and the committed golden vectors.
+
+Bit-exact for every byte (GF(2^8) is integer work; no tolerance).
+"""
+import numpy as np
+import pytest
+
+from oracle import np_oracle as npo
+from oracle.oracle import OracleDecoder
+from tests.conftest import hexarr
+from tests.gpu_util import MUL, dev, host, np_matmul
+
+pytestmark = pytest.mark.gpu
+
+S = ["Ok", "CodingVectorLengthMismatch", "DataLengthMismatch", "PieceCountZero", "DataLengthZero",
+     "PieceLengthZero", "NotEnoughPiecesToRecode", "PieceLengthTooShort", "PieceNotUseful", "ReceivedAllPieces",
+     "NotAllPiecesReceivedYet", "InvalidDecodedDataFormat", "InvalidPieceLength", "InvalidOutputBuffer"]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    import rlnc_amd
+
+    c = rlnc_amd.Context(0)
+    yield c
+    c.set_kernel_variant(0, 0)
+
+
+# ------------------------------------------------------------------------------------------------
+# L1 primitives (simd/mod.rs:18-119): all scalars incl. the 0/1 early-outs, aligned and unaligned
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n,off", [(1, 0), (15, 0), (16, 0), (17, 3), (1000, 1), (4096, 0), (65537, 5),
+                                   (1 << 20, 0)])
+def test_primitives(ctx, n, off):
+    import torch
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(n + off)
+    a = rng.integers(0, 256, n, dtype=np.uint8)
+    b = rng.integers(0, 256, n, dtype=np.uint8)
+    for c in [0, 1, 2, 0x53, 0x80, 0xFF]:
+        ta = torch.zeros(n + off, dtype=torch.uint8, device="cuda:0")
+        tb = torch.zeros(n + off, dtype=torch.uint8, device="cuda:0")
+        ta[off:] = dev(a)
+        tb[off:] = dev(b)
+        va, vb = ta[off:], tb[off:]
+        batch.mul_vec_by_scalar(va, c, ctx)
+        assert np.array_equal(host(va), MUL[c][a]), c
+        ta[off:] = dev(a)
+        batch.mul_vec_by_scalar_then_add_into_vec(vb, va, c, ctx)
+        assert np.array_equal(host(vb), b ^ MUL[c][a]), c
+        tb[off:] = dev(b)
+        batch.add_vectors(vb, va, ctx)
+        assert np.array_equal(host(vb), a ^ b)
+
+
+# ------------------------------------------------------------------------------------------------
+# the matrix operator: shapes around every tile/row/column boundary, both kernel variants
+# ------------------------------------------------------------------------------------------------
+SHAPES = [(1, 1, 1, 1), (1, 3, 17, 1), (2, 2, 16, 2), (3, 5, 4095, 1), (4, 32, 4096, 2), (5, 33, 4097, 1),
+          (8, 7, 100, 3), (16, 16, 8192, 1), (17, 31, 5000, 2), (32, 32, 12288, 1), (33, 64, 4096, 1),
+          (64, 32, 4096 * 3 + 48, 1), (70, 65, 333, 2)]
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("n_out,n_in,W,nobj", SHAPES)
+def test_matmul(ctx, variant, n_out, n_in, W, nobj):
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(n_out * 1000 + n_in * 10 + W + nobj)
+    coef = rng.integers(0, 256, (nobj, n_out, n_in), dtype=np.uint8)
+    coef[:, 0, :] = 1
+    if n_out > 1:
+        coef[:, 1, ::2] = 0
+    inp = rng.integers(0, 256, (nobj, n_in, W), dtype=np.uint8)
+    out = dev(np.zeros((nobj, n_out, W), np.uint8))
+    ctx.set_kernel_variant(variant, 0)
+    try:
+        batch.matmul(dev(coef), dev(inp), out, ctx)
+        got = host(out)
+    finally:
+        ctx.set_kernel_variant(0, 0)
+    for o in range(nobj):
+        assert np.array_equal(got[o], np_matmul(coef[o], inp[o])), o
+
+
+@pytest.mark.parametrize("tile", [1, 2, 4, 8, 16, 32])
+def test_matmul_tile_caps(ctx, tile):
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(tile)
+    coef = rng.integers(0, 256, (1, 40, 12), dtype=np.uint8)
+    inp = rng.integers(0, 256, (1, 12, 4096 + 16), dtype=np.uint8)
+    out = dev(np.zeros((1, 40, 4096 + 16), np.uint8))
+    ctx.set_kernel_variant(0, tile)
+    try:
+        batch.matmul(dev(coef), dev(inp), out, ctx)
+        got = host(out)
+    finally:
+        ctx.set_kernel_variant(0, 0)
+    assert np.array_equal(got[0], np_matmul(coef[0], inp[0]))
+
+
+# ------------------------------------------------------------------------------------------------
+# golden vectors through the object API (rlnc::full mirror → C ABI)
+# ------------------------------------------------------------------------------------------------
+def test_golden_encode(ctx, golden):
+    from rlnc_amd.full import Encoder
+
+    for v in golden["encode"]:
+        k, L, n = v["k"], v["L"], v["n"]
+        enc = Encoder.without_padding(hexarr(v["src"]), k, ctx=ctx)
+        co = hexarr(v["coeffs"]).reshape(n, k)
+        want = hexarr(v["out"]).reshape(n, k + L)
+        for i in range(n):
+            full = np.zeros(k + L, np.uint8)
+
+            class R:  # the "rng" hands out the committed coefficient row
+                def fill_bytes(self, m, row=co[i]):
+                    return row[:m].tobytes()
+
+            enc.code_with_buf(R(), full)
+            assert np.array_equal(full, want[i]), (k, L, i)
+
+
+def test_golden_pad(ctx, golden):
+    from rlnc_amd.full import Encoder
+
+    for v in golden["pad"]:
+        k, L = v["k"], v["L"]
+        enc = Encoder.new(hexarr(v["data"]), k, ctx=ctx)
+        assert enc.get_piece_byte_len() == L and enc.get_full_coded_piece_byte_len() == k + L
+        rows = []
+        for i in range(k):  # unit coding vectors read the padded pieces back
+            out = np.zeros(L, np.uint8)
+            cv = np.zeros(k, np.uint8)
+            cv[i] = 1
+            enc.code_with_coding_vector(cv, out)
+            rows.append(out)
+        assert np.concatenate(rows).tobytes().hex() == v["padded"]
+
+
+def test_golden_recode(ctx, golden):
+    from rlnc_amd.full import Recoder
+
+    for v in golden["recode"]:
+        k, L, n = v["k"], v["L"], v["n"]
+        rec = Recoder.new(hexarr(v["pieces"]), k + L, k, ctx=ctx)
+        assert rec.get_num_pieces_recoded_together() == n and rec.get_piece_byte_len() == L
+        out = np.zeros(k + L, np.uint8)
+        rec.recode_with_coding_vector(hexarr(v["r"]), out)
+        assert out.tobytes().hex() == v["out"]
+
+
+def test_golden_decode_object_api(ctx, golden):
+    from rlnc_amd.full import Decoder
+    from rlnc_amd.errors import RLNCError
+
+    for v in golden["decode"]:
+        d = Decoder.new(v["L"], v["k"], ctx=ctx)
+        sts = []
+        for p in v["pieces"]:
+            try:
+                d.decode(hexarr(p))
+                sts.append("Ok")
+            except RLNCError as e:
+                sts.append(e.name)
+        assert sts == v["statuses"], v["name"]
+        try:
+            data = d.get_decoded_data()
+            assert v["final_status"] == "Ok" and data.tobytes().hex() == v["data"], v["name"]
+        except RLNCError as e:
+            assert e.name == v["final_status"], v["name"]
+
+
+def test_golden_decode_batch(ctx, golden):
+    from rlnc_amd import batch
+
+    for v in golden["decode"]:
+        k, L = v["k"], v["L"]
+        ps = [hexarr(p) for p in v["pieces"]]
+        if any(p.size != k + L for p in ps):
+            continue
+        pieces = dev(np.stack(ps)[None])
+        decoded = dev(np.zeros((1, k, L), np.uint8))
+        pst, ost, dl = batch.decode_batch(pieces, k, decoded, ctx)
+        assert [S[s] for s in pst[0]] == v["statuses"], v["name"]
+        got = host(decoded)[0]
+        assert got[: v["rows"]].tobytes().hex() == v["payload"], v["name"]
+        assert S[ost[0]] == v["final_status"], v["name"]
+        if v["final_status"] == "Ok":
+            assert got.reshape(-1)[: dl[0]].tobytes().hex() == v["data"]
+
+
+# ------------------------------------------------------------------------------------------------
+# ports of src/full/tests.rs (round trips with random sizes, recoders, useless pieces)
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("seed", range(4))
+def test_prop_encoder_decoder(ctx, seed):
+    # full/tests.rs:7-47
+    from rlnc_amd.errors import RLNCError
+    from rlnc_amd.full import Decoder, Encoder
+
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 256, int(rng.integers(1 << 10, 1 << 16)), dtype=np.uint8)
+    k = int(rng.integers(1 << 5, 1 << 8))
+    enc = Encoder.new(data, k, ctx=ctx)
+    dec = Decoder.new(enc.get_piece_byte_len(), enc.get_piece_count(), ctx=ctx)
+    while True:
+        try:
+            dec.decode(enc.code(rng))
+        except RLNCError as e:
+            if e == RLNCError.ReceivedAllPieces:
+                break
+            assert e == RLNCError.PieceNotUseful
+    assert dec.is_already_decoded()
+    assert np.array_equal(dec.get_decoded_data(), data)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_prop_encoder_recoder_decoder(ctx, seed):
+    # full/tests.rs:49-119 (counts reduced)
+    from rlnc_amd.errors import RLNCError
+    from rlnc_amd.full import Decoder, Encoder, Recoder
+
+    rng = np.random.default_rng(10 + seed)
+    data = rng.integers(0, 256, int(rng.integers(1 << 10, 1 << 15)), dtype=np.uint8)
+    k = int(rng.integers(1 << 5, 1 << 7))
+    enc = Encoder.new(data, k, ctx=ctx)
+    dec = Decoder.new(enc.get_piece_byte_len(), enc.get_piece_count(), ctx=ctx)
+    done = False
+    while not done:
+        nrec = int(rng.integers(2, k))
+        coded = np.concatenate([enc.code(rng) for _ in range(nrec)])
+        rec = Recoder.new(coded, enc.get_full_coded_piece_byte_len(), enc.get_piece_count(), ctx=ctx)
+        for _ in range(int(rng.integers(0, 2 * k))):
+            try:
+                dec.decode(rec.recode(rng))
+            except RLNCError as e:
+                if e == RLNCError.ReceivedAllPieces:
+                    done = True
+                    break
+                assert e == RLNCError.PieceNotUseful
+        if done:
+            break
+        try:
+            dec.decode(enc.code(rng))
+        except RLNCError as e:
+            if e == RLNCError.ReceivedAllPieces:
+                break
+            assert e == RLNCError.PieceNotUseful
+    assert np.array_equal(dec.get_decoded_data(), data)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_prop_decoding_with_useless_pieces(ctx, seed):
+    # full/tests.rs:121-203
+    from rlnc_amd.errors import RLNCError
+    from rlnc_amd.full import Decoder, Encoder, Recoder
+
+    rng = np.random.default_rng(20 + seed)
+    data = rng.integers(0, 256, int(rng.integers(1 << 10, 1 << 16)), dtype=np.uint8)
+    k = int(rng.integers(1 << 5, 1 << 8))
+    enc = Encoder.new(data, k, ctx=ctx)
+    dec = Decoder.new(enc.get_piece_byte_len(), enc.get_piece_count(), ctx=ctx)
+    seen = []
+    for _ in range(k // 2):
+        p = enc.code(rng)
+        try:
+            dec.decode(p)
+            seen.append(p)
+        except RLNCError as e:
+            assert e == RLNCError.PieceNotUseful
+    rec = Recoder.new(np.concatenate(seen), enc.get_full_coded_piece_byte_len(), enc.get_piece_count(), ctx=ctx)
+    for _ in range(2 * len(seen)):
+        with pytest.raises(RLNCError) as ei:
+            dec.decode(rec.recode(rng))
+        assert ei.value == RLNCError.PieceNotUseful
+    while dec.get_remaining_piece_count() > 0:
+        try:
+            dec.decode(enc.code(rng))
+        except RLNCError as e:
+            assert e == RLNCError.PieceNotUseful
+    assert np.array_equal(dec.get_decoded_data(), data)
+
+
+# ------------------------------------------------------------------------------------------------
+# BASELINE.json configs at full size, bit-exact against the C oracle
+# ------------------------------------------------------------------------------------------------
+def test_config2_encode_32x1MiB_to_64(ctx, orc):
+    from rlnc_amd import batch
+
+    k, L, n = 32, 1 << 20, 64
+    rng = np.random.default_rng(0x524C4E43)
+    src = rng.integers(0, 256, (1, k, L), dtype=np.uint8)
+    co = rng.integers(0, 256, (1, n, k), dtype=np.uint8)
+    out = dev(np.zeros((1, n, k + L), np.uint8))
+    batch.encode_batch(dev(src), dev(co), out, ctx)
+    got = host(out)[0]
+    assert np.array_equal(got, orc.encode(src[0], co[0]))
+
+
+def test_config3_decode_32x1MiB(ctx, orc):
+    from rlnc_amd import batch
+
+    k, L = 32, 1 << 20
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, k * L - 1, dtype=np.uint8)  # Encoder::new pads to exactly L = 2^20
+    src = orc.pad(data, k)
+    assert src.shape == (k, L)
+    co = rng.integers(0, 256, (k + 2, k), dtype=np.uint8)
+    coded = orc.encode(src, co)
+    pieces = dev(coded[None])
+    decoded = dev(np.zeros((1, k, L), np.uint8))
+    pst, ost, dl = batch.decode_batch(pieces, k, decoded, ctx)
+    od = OracleDecoder(L, k)
+    want = [S[od.decode(p)] for p in coded]
+    assert [S[s] for s in pst[0]] == want
+    got = host(decoded)[0]
+    assert np.array_equal(got, od.padded_payload())
+    assert S[ost[0]] == "Ok" and int(dl[0]) == data.size
+    assert np.array_equal(got.reshape(-1)[: data.size], data)
+
+
+def test_config4_recode_64x256KiB(ctx, orc):
+    from rlnc_amd import batch
+
+    k, L, n, count = 64, 1 << 18, 64, 64
+    rng = np.random.default_rng(4)
+    src = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    pieces = orc.encode(src, rng.integers(0, 256, (n, k), dtype=np.uint8))
+    r = rng.integers(0, 256, (1, count, n), dtype=np.uint8)
+    out = dev(np.zeros((1, count, k + L), np.uint8))
+    batch.recode_batch(dev(pieces[None]), dev(r), out, k, ctx)
+    got = host(out)[0]
+    for c in [0, 1, count - 1]:
+        assert np.array_equal(got[c], orc.recode(pieces, k + L, k, r[0, c]))
+    # all 64 at once against the independent numpy matmul on a column slice
+    assert np.array_equal(got[:, :4096 + k], np_matmul(r[0], pieces[:, :4096 + k]))
+
+
+def test_config5_batch_objects_k128_64KiB(ctx, orc):
+    from rlnc_amd import batch
+
+    k, L, nobj = 128, 1 << 16, 8
+    rng = np.random.default_rng(5)
+    src = rng.integers(0, 256, (nobj, k, L), dtype=np.uint8)
+    co = rng.integers(0, 256, (nobj, k, k), dtype=np.uint8)
+    pieces = dev(np.zeros((nobj, k, k + L), np.uint8))
+    batch.encode_batch(dev(src), dev(co), pieces, ctx)
+    hp = host(pieces)
+    assert np.array_equal(hp[0], orc.encode(src[0], co[0]))
+    decoded = dev(np.zeros((nobj, k, L), np.uint8))
+    pst, ost, dl = batch.decode_batch(pieces, k, decoded, ctx)
+    got = host(decoded)
+    od = OracleDecoder(L, k)
+    want = [S[od.decode(p)] for p in hp[1]]
+    assert [S[s] for s in pst[1]] == want
+    assert np.array_equal(got[1], od.padded_payload())
+    for o in range(nobj):
+        if (pst[o] == 0).sum() == k:  # full rank: decode must return the source rows
+            assert np.array_equal(got[o], src[o])
