@@ -62,8 +62,11 @@ const char *rlnc_version(void);
 typedef struct rlnc_context rlnc_context;
 int rlnc_context_create(int device, rlnc_context **out);
 void rlnc_context_destroy(rlnc_context *ctx);
-/* Use an external hipStream_t (NULL = the context's own stream).  The caller keeps ownership. */
+/* Launch on an external hipStream_t, taken literally: NULL is HIP's null (default) stream, which is what
+ * torch.cuda.current_stream().cuda_stream returns for torch's default stream.  The caller keeps ownership. */
 int rlnc_context_set_stream(rlnc_context *ctx, void *hip_stream);
+/* Go back to the context's own non-blocking stream (the initial state). */
+int rlnc_context_use_own_stream(rlnc_context *ctx);
 void *rlnc_context_get_stream(rlnc_context *ctx);
 int rlnc_context_synchronize(rlnc_context *ctx);
 int rlnc_context_device(const rlnc_context *ctx);
@@ -99,6 +102,9 @@ int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc);
  * default), 1 = nibble (the reference's 4-bit split LOW/HIGH tables looked up from LDS byte-wise).
  * max_tile_rows caps the output rows per workgroup (0 = automatic, else 1/2/4/8/16/32). */
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows);
+/* Where rlnc_decode_batch runs the coefficient elimination: 0 = auto (device when it fits LDS, default),
+ * 1 = host threads, 2 = device.  Both are exact replicas; the switch exists for A/B tests. */
+int rlnc_set_decode_path(rlnc_context *ctx, int path);
 
 /* ---- Encoder: src/full/encoder.rs ----------------------------------------------------------------- */
 typedef struct rlnc_encoder rlnc_encoder;
@@ -187,6 +193,13 @@ int rlnc_recode_batch(rlnc_context *ctx, const uint8_t *pieces_dev, size_t k, si
 int rlnc_decode_batch(rlnc_context *ctx, const uint8_t *pieces_dev, size_t pieces_obj_stride, size_t k, size_t L,
                       size_t m, size_t num_objects, uint8_t *decoded_dev, int32_t *piece_status,
                       int32_t *object_status, uint64_t *data_len);
+
+/* Fully asynchronous variant: everything stays on the device (statuses int32 [obj][m] and [obj], unpadded
+ * lengths int64 [obj], all device pointers).  The exact elimination runs on the device (one wave per
+ * object, LDS-resident [coeffs | E]; requires (k+1)·4·ceil_pow2((k+m)/4) + 8 KiB <= 160 KiB). */
+int rlnc_decode_batch_device(rlnc_context *ctx, const uint8_t *pieces_dev, size_t pieces_obj_stride, size_t k,
+                             size_t L, size_t m, size_t num_objects, uint8_t *decoded_dev, int32_t *piece_status_dev,
+                             int32_t *object_status_dev, int64_t *data_len_dev);
 
 /* ---- host-only: the decoder's exact coefficient elimination (no device needed) ---------------------------
  * The diagonal-pivot RREF of DecoderMatrix (decoder_matrix.rs:99-244) replicated on [coeffs | E] where E

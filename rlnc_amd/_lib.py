@@ -37,6 +37,7 @@ _SIGS = {
     "rlnc_context_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
     "rlnc_context_destroy": (None, [vp]),
     "rlnc_context_set_stream": (C.c_int, [vp, vp]),
+    "rlnc_context_use_own_stream": (C.c_int, [vp]),
     "rlnc_context_get_stream": (vp, [vp]),
     "rlnc_context_synchronize": (C.c_int, [vp]),
     "rlnc_context_device": (C.c_int, [vp]),
@@ -45,6 +46,7 @@ _SIGS = {
     "rlnc_gf256_mul_vec_by_scalar_then_add_into_vec": (C.c_int, [vp, vp, vp, C.c_size_t, C.c_uint8]),
     "rlnc_gf256_matmul": (C.c_int, [vp, C.POINTER(MatmulDesc)]),
     "rlnc_set_kernel_variant": (C.c_int, [vp, C.c_int, C.c_int]),
+    "rlnc_set_decode_path": (C.c_int, [vp, C.c_int]),
     "rlnc_encoder_new": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.POINTER(vp)]),
     "rlnc_encoder_without_padding": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.POINTER(vp)]),
     "rlnc_encoder_from_device": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.POINTER(vp)]),
@@ -80,6 +82,8 @@ _SIGS = {
     "rlnc_recode_batch": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp, C.c_size_t, vp]),
     "rlnc_decode_batch": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp, i32p,
                                     i32p, u64p]),
+    "rlnc_decode_batch_device": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp,
+                                           vp, vp, vp]),
     "rlnc_elimination_new": (C.c_int, [C.c_size_t, C.c_size_t, C.POINTER(vp)]),
     "rlnc_elimination_free": (None, [vp]),
     "rlnc_elimination_push": (C.c_int, [vp, vp, i32p, i32p]),
@@ -101,6 +105,13 @@ def load():
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(hipcc --offload-arch=gfx950). rlnc_amd has no CPU fallback.")
+    try:
+        # torch (plumbing for HBM/streams) bundles its own libamdhip64.so.7 — the same SONAME as
+        # /opt/rocm's.  Whichever is loaded first serves the whole process; loading torch's first keeps a
+        # single HIP runtime (loading ours first leaves torch with no visible GPU).
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
         f = getattr(lib, name)

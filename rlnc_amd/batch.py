@@ -65,17 +65,38 @@ def decode_batch(pieces, k: int, decoded, ctx: Context | None = None):
     nobj, m, full = pieces.shape
     L = full - k
     assert pieces.is_cuda and pieces.dtype == torch.uint8
-    assert pieces.stride(2) == 1 and pieces.stride(1) == full and pieces.stride(0) >= m * full
+    # strides of size-1 dimensions are arbitrary in torch; only real ones are checked
+    obj_stride = pieces.stride(0) if nobj > 1 else m * full
+    assert (full == 1 or pieces.stride(2) == 1) and (m == 1 or pieces.stride(1) == full) and obj_stride >= m * full
     _chk(decoded, (nobj, k, L))
     ctx = _ctx_for(pieces, ctx)
     ps = np.zeros((nobj, m), np.int32)
     os_ = np.zeros(nobj, np.int32)
     dl = np.zeros(nobj, np.uint64)
-    check(ctx.lib.rlnc_decode_batch(ctx.h, C.c_void_p(pieces.data_ptr()), pieces.stride(0), k, L, m, nobj,
+    check(ctx.lib.rlnc_decode_batch(ctx.h, C.c_void_p(pieces.data_ptr()), obj_stride, k, L, m, nobj,
                                     C.c_void_p(decoded.data_ptr()),
                                     ps.ctypes.data_as(C.POINTER(C.c_int32)), os_.ctypes.data_as(C.POINTER(C.c_int32)),
                                     dl.ctypes.data_as(C.POINTER(C.c_uint64))), ctx.lib)
     return ps, os_, dl
+
+
+def decode_batch_device(pieces, k: int, decoded, piece_status, object_status, data_len, ctx: Context | None = None):
+    """Asynchronous decode_batch with device outputs: piece_status int32 [obj][m], object_status int32 [obj],
+    data_len int64 [obj] (all device tensors)."""
+    import torch
+
+    nobj, m, full = pieces.shape
+    L = full - k
+    obj_stride = pieces.stride(0) if nobj > 1 else m * full
+    assert (m == 1 or pieces.stride(1) == full) and obj_stride >= m * full
+    _chk(decoded, (nobj, k, L))
+    assert piece_status.dtype == torch.int32 and tuple(piece_status.shape) == (nobj, m)
+    assert object_status.dtype == torch.int32 and data_len.dtype == torch.int64
+    ctx = _ctx_for(pieces, ctx)
+    check(ctx.lib.rlnc_decode_batch_device(ctx.h, C.c_void_p(pieces.data_ptr()), obj_stride, k, L, m, nobj,
+                                           C.c_void_p(decoded.data_ptr()), C.c_void_p(piece_status.data_ptr()),
+                                           C.c_void_p(object_status.data_ptr()), C.c_void_p(data_len.data_ptr())),
+          ctx.lib)
 
 
 def matmul(coef, inp, out, ctx: Context | None = None) -> None:

@@ -31,9 +31,12 @@ class Context:
         except Exception:
             pass
 
-    def set_stream(self, hip_stream_handle: int | None):
-        """Launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)."""
-        check(self.lib.rlnc_context_set_stream(self.h, C.c_void_p(hip_stream_handle or 0)), self.lib)
+    def set_stream(self, hip_stream_handle: int):
+        """Launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream; 0 = null stream)."""
+        check(self.lib.rlnc_context_set_stream(self.h, C.c_void_p(hip_stream_handle)), self.lib)
+
+    def use_own_stream(self):
+        check(self.lib.rlnc_context_use_own_stream(self.h), self.lib)
 
     def use_torch_stream(self):
         import torch
@@ -42,6 +45,10 @@ class Context:
 
     def synchronize(self):
         check(self.lib.rlnc_context_synchronize(self.h), self.lib)
+
+    def set_decode_path(self, path: int = 0):
+        """0 auto, 1 host elimination, 2 device elimination (both exact)."""
+        check(self.lib.rlnc_set_decode_path(self.h, int(path)), self.lib)
 
     def set_kernel_variant(self, variant: int = 0, max_tile_rows: int = 0):
         """variant 0 = perm (v_perm_b32 3-bit split, default), 1 = nibble (4-bit LDS tables)."""

@@ -104,7 +104,8 @@ struct rlnc_context {
     hipStream_t stream = nullptr;
     rlnc::MatmulVariant variant = rlnc::MatmulVariant::Perm;
     int max_tile_rows = 0;
-    DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len;
+    int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination
+    DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len, ws_pstat, ws_rank;
     PinBuf pin_a, pin_b, pin_c;
 
     int activate() const {
@@ -295,7 +296,13 @@ void rlnc_context_destroy(rlnc_context *ctx) {
 
 int rlnc_context_set_stream(rlnc_context *ctx, void *s) {
     CHECK_ARG(ctx != nullptr);
-    ctx->stream = s ? static_cast<hipStream_t>(s) : ctx->own;
+    ctx->stream = static_cast<hipStream_t>(s);
+    return RLNC_OK;
+}
+
+int rlnc_context_use_own_stream(rlnc_context *ctx) {
+    CHECK_ARG(ctx != nullptr);
+    ctx->stream = ctx->own;
     return RLNC_OK;
 }
 
@@ -305,6 +312,12 @@ int rlnc_context_device(const rlnc_context *ctx) { return ctx ? ctx->device : -1
 int rlnc_context_synchronize(rlnc_context *ctx) {
     CHECK_ARG(ctx != nullptr);
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RLNC_OK;
+}
+
+int rlnc_set_decode_path(rlnc_context *ctx, int path) {
+    CHECK_ARG(ctx != nullptr && path >= 0 && path <= 2);
+    ctx->decode_path = path;
     return RLNC_OK;
 }
 
@@ -788,19 +801,52 @@ int rlnc_recode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t k, size_t
     return ctx->matmul(p);
 }
 
-int rlnc_decode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L, size_t m,
-                      size_t nobj, uint8_t *decoded, int32_t *piece_status, int32_t *object_status,
-                      uint64_t *data_len) {
-    CHECK_ARG(ctx != nullptr);
-    if (L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;
-    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
-    if (nobj == 0) return RLNC_OK;
-    CHECK_ARG(pieces && decoded && m > 0 && m <= 0x7FFFFFFF && k <= 0x7FFFFFFF && nobj <= 0x7FFFFFFF);
-    int st = ctx->activate();
-    if (st) return st;
+// Device path: exact elimination on the device (rref.hip) → T × data (one matmul) → marker scan.
+// Everything is enqueued on the context stream; outputs stay on the device.
+static int decode_batch_device_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
+                                    size_t m, size_t nobj, uint8_t *decoded, int32_t *pstat_dev, int32_t *ostat_dev,
+                                    int64_t *len_dev, int32_t *rank_dev) {
     const size_t full = k + L;
-    if (obj_stride == 0) obj_stride = m * full;
-    CHECK_ARG(obj_stride >= m * full);
+    int st;
+    if ((st = ctx->ws_coef.ensure(nobj * k * m)) || (st = ctx->ws_scan.ensure(nobj * 8))) return st;
+    rlnc::RrefParams rp{};
+    rp.pieces = pieces;
+    rp.obj_stride = int64_t(obj_stride);
+    rp.piece_stride = int64_t(full);
+    rp.k = int(k);
+    rp.m = int(m);
+    rp.n_obj = int(nobj);
+    rp.T = ctx->ws_coef.as<uint8_t>();
+    rp.T_obj = int64_t(k * m);
+    rp.status = pstat_dev;
+    rp.rank = rank_dev;
+    HIP_TRY(rlnc::launch_rref_batch(rp, ctx->stream));
+    rlnc::MatmulParams p{};
+    p.in = pieces + k;
+    p.in_obj = int64_t(obj_stride);
+    p.in_row = int64_t(full);
+    p.coef = ctx->ws_coef.as<uint8_t>();
+    p.coef_obj = int64_t(k * m);
+    p.coef_row = int64_t(m);
+    p.out = decoded;
+    p.out_obj = int64_t(k * L);
+    p.out_row = int64_t(L);
+    p.n_out = int(k);
+    p.n_in = int(m);
+    p.width = int64_t(L);
+    p.n_obj = int(nobj);
+    if ((st = ctx->matmul(p))) return st;
+    HIP_TRY(rlnc::launch_final_data_len_ranked(decoded, int64_t(k * L), int64_t(k * L), int(nobj), int(k), rank_dev,
+                                               ctx->ws_scan.as<unsigned long long>(), ostat_dev, len_dev, ctx->stream));
+    return RLNC_OK;
+}
+
+// Host path (matrices too large for LDS): exact elimination on host threads (elimination.hpp).
+static int decode_batch_host_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
+                                  size_t m, size_t nobj, uint8_t *decoded, int32_t *piece_status, int32_t *object_status,
+                                  uint64_t *data_len) {
+    const size_t full = k + L;
+    int st;
     // 1. coefficient headers → host (k bytes of each piece)
     if ((st = ctx->pin_a.ensure(nobj * m * k))) return st;
     uint8_t *hdr = ctx->pin_a.as<uint8_t>();
@@ -844,8 +890,12 @@ int rlnc_decode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t obj_strid
         for (auto &t : th) t.join();
     }
     // 3. T → device, decoded = T × received data rows (one launch for all objects)
-    if ((st = ctx->ws_coef.ensure(nobj * k * m))) return st;
+    if ((st = ctx->ws_coef.ensure(nobj * k * m)) || (st = ctx->ws_rank.ensure(nobj * 4)) ||
+        (st = ctx->ws_scan.ensure(nobj * 8)) || (st = ctx->ws_status.ensure(nobj * 4)) ||
+        (st = ctx->ws_len.ensure(nobj * 8)) || (st = ctx->pin_c.ensure(nobj * 16)))
+        return st;
     HIP_TRY(hipMemcpyAsync(ctx->ws_coef.p, T, nobj * k * m, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->ws_rank.p, ranks.data(), nobj * 4, hipMemcpyHostToDevice, ctx->stream));
     rlnc::MatmulParams p{};
     p.in = pieces + k;
     p.in_obj = int64_t(obj_stride);
@@ -862,24 +912,79 @@ int rlnc_decode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t obj_strid
     p.n_obj = int(nobj);
     if ((st = ctx->matmul(p))) return st;
     // 4. get_final_data_len on device (decoder.rs:162-177)
-    if ((st = ctx->ws_scan.ensure(nobj * 8)) || (st = ctx->ws_status.ensure(nobj * 4)) ||
-        (st = ctx->ws_len.ensure(nobj * 8)) || (st = ctx->pin_c.ensure(nobj * 16)))
-        return st;
-    HIP_TRY(rlnc::launch_final_data_len(decoded, int64_t(k * L), int64_t(k * L), int(nobj),
-                                        ctx->ws_scan.as<unsigned long long>(), ctx->ws_status.as<int32_t>(),
-                                        ctx->ws_len.as<int64_t>(), RLNC_ERR_INVALID_DECODED_DATA_FORMAT, ctx->stream));
+    HIP_TRY(rlnc::launch_final_data_len_ranked(decoded, int64_t(k * L), int64_t(k * L), int(nobj), int(k),
+                                               ctx->ws_rank.as<int32_t>(), ctx->ws_scan.as<unsigned long long>(),
+                                               ctx->ws_status.as<int32_t>(), ctx->ws_len.as<int64_t>(), ctx->stream));
     int32_t *hst = ctx->pin_c.as<int32_t>();
     int64_t *hlen = reinterpret_cast<int64_t *>(ctx->pin_c.as<uint8_t>() + nobj * 8);
     HIP_TRY(hipMemcpyAsync(hst, ctx->ws_status.p, nobj * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipMemcpyAsync(hlen, ctx->ws_len.p, nobj * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     for (size_t o = 0; o < nobj; ++o) {
-        const bool done = size_t(ranks[o]) == k;
-        if (object_status) object_status[o] = done ? hst[o] : RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;
-        if (data_len) data_len[o] = (done && hst[o] == 0) ? uint64_t(hlen[o]) : 0;
+        if (object_status) object_status[o] = hst[o];
+        if (data_len) data_len[o] = uint64_t(hlen[o]);
     }
     if (piece_status) std::memcpy(piece_status, pst.data(), nobj * m * sizeof(int32_t));
     return RLNC_OK;
+}
+
+static int decode_batch_check(rlnc_context *ctx, const uint8_t *pieces, size_t &obj_stride, size_t k, size_t L,
+                              size_t m, size_t nobj, uint8_t *decoded) {
+    CHECK_ARG(ctx != nullptr);
+    if (L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
+    CHECK_ARG(pieces && decoded && m > 0 && m <= 0x7FFFFFFF && k <= 0x7FFFFFFF && nobj <= 0x7FFFFFFF);
+    if (obj_stride == 0) obj_stride = m * (k + L);
+    CHECK_ARG(obj_stride >= m * (k + L));
+    return ctx->activate();
+}
+
+int rlnc_decode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L, size_t m,
+                      size_t nobj, uint8_t *decoded, int32_t *piece_status, int32_t *object_status,
+                      uint64_t *data_len) {
+    if (nobj == 0 && ctx) return RLNC_OK;
+    int st = decode_batch_check(ctx, pieces, obj_stride, k, L, m, nobj, decoded);
+    if (st) return st;
+    const bool fits = rlnc::rref_lds_bytes(int(k), int(m)) <= rlnc::kRrefMaxLds;
+    if (ctx->decode_path == 2 && !fits)
+        return set_error(RLNC_ERR_INVALID_ARGUMENT, "device elimination forced but k=%zu, m=%zu exceed LDS", k, m);
+    if (!fits || ctx->decode_path == 1)
+        return decode_batch_host_impl(ctx, pieces, obj_stride, k, L, m, nobj, decoded, piece_status, object_status,
+                                      data_len);
+    if ((st = ctx->ws_pstat.ensure(nobj * m * 4)) || (st = ctx->ws_status.ensure(nobj * 4)) ||
+        (st = ctx->ws_len.ensure(nobj * 8)) || (st = ctx->ws_rank.ensure(nobj * 4)) ||
+        (st = ctx->pin_c.ensure(nobj * (m * 4 + 16))))
+        return st;
+    if ((st = decode_batch_device_impl(ctx, pieces, obj_stride, k, L, m, nobj, decoded, ctx->ws_pstat.as<int32_t>(),
+                                       ctx->ws_status.as<int32_t>(), ctx->ws_len.as<int64_t>(),
+                                       ctx->ws_rank.as<int32_t>())))
+        return st;
+    uint8_t *h = ctx->pin_c.as<uint8_t>();
+    HIP_TRY(hipMemcpyAsync(h, ctx->ws_status.p, nobj * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(h + nobj * 8, ctx->ws_len.p, nobj * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(h + nobj * 16, ctx->ws_pstat.p, nobj * m * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (size_t o = 0; o < nobj; ++o) {
+        if (object_status) object_status[o] = reinterpret_cast<int32_t *>(h)[o];
+        if (data_len) data_len[o] = uint64_t(reinterpret_cast<int64_t *>(h + nobj * 8)[o]);
+    }
+    if (piece_status) std::memcpy(piece_status, h + nobj * 16, nobj * m * 4);
+    return RLNC_OK;
+}
+
+int rlnc_decode_batch_device(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L, size_t m,
+                             size_t nobj, uint8_t *decoded, int32_t *piece_status_dev, int32_t *object_status_dev,
+                             int64_t *data_len_dev) {
+    if (nobj == 0 && ctx) return RLNC_OK;
+    int st = decode_batch_check(ctx, pieces, obj_stride, k, L, m, nobj, decoded);
+    if (st) return st;
+    CHECK_ARG(piece_status_dev && object_status_dev && data_len_dev);
+    if (rlnc::rref_lds_bytes(int(k), int(m)) > rlnc::kRrefMaxLds)
+        return set_error(RLNC_ERR_INVALID_ARGUMENT, "k=%zu, m=%zu exceed the device elimination's LDS budget; use "
+                         "rlnc_decode_batch", k, m);
+    if ((st = ctx->ws_rank.ensure(nobj * 4))) return st;
+    return decode_batch_device_impl(ctx, pieces, obj_stride, k, L, m, nobj, decoded, piece_status_dev,
+                                    object_status_dev, data_len_dev, ctx->ws_rank.as<int32_t>());
 }
 
 // ------------------------------------------------------------------------------------------------------

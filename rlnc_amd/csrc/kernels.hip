@@ -19,6 +19,7 @@
 // north-star's literal design; it is kept as the ablation baseline.
 #include <hip/hip_runtime.h>
 
+#include "../../include/rlnc_hip.h"
 #include "gf256.hpp"
 #include "kernels.hpp"
 
@@ -306,27 +307,36 @@ hipError_t launch_vec(uint8_t *dst, const uint8_t *src, int64_t len, uint8_t c, 
 // get_final_data_len on device (decoder.rs:162-177).  Equivalent formulation: the last nonzero byte of
 // the padded payload must be the boundary marker and must not sit at index 0.
 // ---------------------------------------------------------------------------------------------------
+// One wave per object scans 1 KiB chunks from the END of the payload: for any padded object the last
+// nonzero byte lies in the final k bytes (Encoder::new pads with < k zeros after the marker,
+// encoder.rs:95-99), so the scan normally stops after one chunk — O(1) instead of a full re-read.
 template <bool ALIGNED>
-__global__ __launch_bounds__(kThreads) void last_nonzero_kernel(const uint8_t *data, int64_t obj_stride, int64_t len,
-                                                                unsigned long long *best) {
-    const int obj = blockIdx.y;
+__global__ __launch_bounds__(64) void last_nonzero_kernel(const uint8_t *data, int64_t obj_stride, int64_t len,
+                                                          unsigned long long *best) {
+    const int obj = blockIdx.x;
+    const int lane = threadIdx.x;
     const uint8_t *d = data + int64_t(obj) * obj_stride;
-    unsigned long long mine = 0;  // index + 1 of the last nonzero byte seen, 0 = none
-    const int64_t stride = int64_t(gridDim.x) * kThreads * kBytesPerThread;
-    for (int64_t off = (int64_t(blockIdx.x) * kThreads + threadIdx.x) * kBytesPerThread; off < len; off += stride) {
-        const int nb = int(min<int64_t>(kBytesPerThread, len - off));
-        const uint4 x = load16<ALIGNED>(d + off, nb);
-        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    for (int64_t c = (len + 1023) / 1024 - 1; c >= 0; --c) {
+        const int64_t off = c * 1024 + int64_t(lane) * kBytesPerThread;
+        unsigned long long mine = 0;  // index + 1 of the last nonzero byte in this lane's 16 B, 0 = none
+        if (off < len) {
+            const int nb = int(min<int64_t>(kBytesPerThread, len - off));
+            const uint4 x = load16<ALIGNED>(d + off, nb);
+            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (w[q]) mine = (unsigned long long)(off + 4 * q + (31 - __builtin_clz(w[q])) / 8 + 1);
+            for (int q = 0; q < 4; ++q)
+                if (w[q]) mine = (unsigned long long)(off + 4 * q + (31 - __builtin_clz(w[q])) / 8 + 1);
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long v = __shfl_xor(mine, o);
+            mine = v > mine ? v : mine;
+        }
+        if (mine) {  // wave-uniform after the reduction
+            if (lane == 0) best[obj] = mine;
+            return;
+        }
     }
-    // wave reduce then one atomic per wave
-    for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long o = __shfl_xor(mine, off);
-        mine = o > mine ? o : mine;
-    }
-    if ((threadIdx.x & 63) == 0 && mine) atomicMax(best + obj, mine);
+    if (lane == 0) best[obj] = 0;
 }
 
 __global__ void final_len_kernel(const uint8_t *data, int64_t obj_stride, int n_obj, const unsigned long long *best,
@@ -340,7 +350,38 @@ __global__ void final_len_kernel(const uint8_t *data, int64_t obj_stride, int n_
     final_len[o] = ok ? idx : 0;
 }
 
+__global__ void final_len_ranked_kernel(const uint8_t *data, int64_t obj_stride, int n_obj, int k, const int32_t *rank,
+                                        const unsigned long long *best, int32_t *status, int64_t *final_len) {
+    const int o = blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= n_obj) return;
+    if (rank[o] < k) {  // decoder.rs:137-139
+        status[o] = RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;
+        final_len[o] = 0;
+        return;
+    }
+    const unsigned long long b = best[o];
+    const int64_t idx = int64_t(b) - 1;
+    const bool ok = b != 0 && idx != 0 && data[int64_t(o) * obj_stride + idx] == kBoundaryMarker;
+    status[o] = ok ? RLNC_OK : RLNC_ERR_INVALID_DECODED_DATA_FORMAT;
+    final_len[o] = ok ? idx : 0;
+}
+
 }  // namespace
+
+hipError_t launch_final_data_len_ranked(const uint8_t *data, int64_t obj_stride, int64_t len, int n_obj, int k,
+                                        const int32_t *rank, unsigned long long *scratch, int32_t *status,
+                                        int64_t *final_len, hipStream_t s) {
+    if (n_obj <= 0) return hipSuccess;
+    if (al16(data) && (n_obj == 1 || al16(obj_stride)))
+        hipLaunchKernelGGL(last_nonzero_kernel<true>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch);
+    else
+        hipLaunchKernelGGL(last_nonzero_kernel<false>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(final_len_ranked_kernel, dim3((n_obj + 255) / 256), dim3(256), 0, s, data, obj_stride, n_obj, k,
+                       rank, scratch, status, final_len);
+    return hipGetLastError();
+}
 
 hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v) {
     if (p.n_out <= 0 || p.width <= 0 || p.n_obj <= 0) return hipSuccess;
@@ -369,14 +410,11 @@ hipError_t launch_final_data_len(const uint8_t *data, int64_t obj_stride, int64_
                                  unsigned long long *scratch, int32_t *status, int64_t *final_len,
                                  int32_t invalid_code, hipStream_t s) {
     if (n_obj <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(scratch, 0, sizeof(unsigned long long) * n_obj, s);
-    if (e != hipSuccess) return e;
-    const int64_t chunks = (len + kBytesPerThread - 1) / kBytesPerThread;
-    const int bx = int(std::min<int64_t>(std::max<int64_t>((chunks + kThreads - 1) / kThreads / 4, 1), 1024));
+    hipError_t e;
     if (al16(data) && (n_obj == 1 || al16(obj_stride)))
-        hipLaunchKernelGGL(last_nonzero_kernel<true>, dim3(bx, n_obj), dim3(kThreads), 0, s, data, obj_stride, len, scratch);
+        hipLaunchKernelGGL(last_nonzero_kernel<true>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch);
     else
-        hipLaunchKernelGGL(last_nonzero_kernel<false>, dim3(bx, n_obj), dim3(kThreads), 0, s, data, obj_stride, len, scratch);
+        hipLaunchKernelGGL(last_nonzero_kernel<false>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(final_len_kernel, dim3((n_obj + 255) / 256), dim3(256), 0, s, data, obj_stride, n_obj, scratch,
                        status, final_len, invalid_code);

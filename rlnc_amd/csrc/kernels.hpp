@@ -44,4 +44,25 @@ hipError_t launch_final_data_len(const uint8_t *data, int64_t obj_stride, int64_
                                  unsigned long long *scratch, int32_t *status, int64_t *final_len,
                                  int32_t invalid_code, hipStream_t s);
 
+// Device replica of Decoder::decode over pieces 0..m-1 of every object (rref.hip).  Piece p of object o
+// starts (coefficient header first) at pieces + o*obj_stride + p*piece_stride.  Outputs: status[o][p]
+// (RLNC status of each decode() call), rank[o], T[o] (k × m, row-major, rows >= rank zero).
+struct RrefParams {
+    const uint8_t *pieces;
+    int64_t obj_stride, piece_stride;
+    int k, m, n_obj;
+    uint8_t *T;
+    int64_t T_obj;
+    int32_t *status;
+    int32_t *rank;
+};
+constexpr size_t kRrefMaxLds = 160 * 1024;
+size_t rref_lds_bytes(int k, int m);
+hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s);
+
+// final_len with the decoder's rank: objects with rank < k report NotAllPiecesReceivedYet
+hipError_t launch_final_data_len_ranked(const uint8_t *data, int64_t obj_stride, int64_t len, int n_obj, int k,
+                                        const int32_t *rank, unsigned long long *scratch, int32_t *status,
+                                        int64_t *final_len, hipStream_t s);
+
 }  // namespace rlnc

@@ -18,6 +18,12 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   if fatal $rc; then echo "fatal rc from pytest; stopping"; exit $rc; fi
 fi
 
+if [ -n "${SWEEP:-}" ]; then
+  timeout -k 10 300 python scripts/sweep.py ${SWEEP} > "$OUT/sweep.jsonl" 2> "$OUT/sweep.err"
+  rc=$?; echo "sweep rc=$rc"; cat "$OUT/sweep.jsonl"; tail -3 "$OUT/sweep.err"
+  if fatal $rc; then exit $rc; fi
+fi
+
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"
 if fatal $rc; then exit $rc; fi

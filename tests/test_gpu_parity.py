@@ -176,9 +176,11 @@ def test_golden_decode_object_api(ctx, golden):
             assert e.name == v["final_status"], v["name"]
 
 
-def test_golden_decode_batch(ctx, golden):
+@pytest.mark.parametrize("path", [1, 2])
+def test_golden_decode_batch(ctx, golden, path):
     from rlnc_amd import batch
 
+    ctx.set_decode_path(path)
     for v in golden["decode"]:
         k, L = v["k"], v["L"]
         ps = [hexarr(p) for p in v["pieces"]]
@@ -193,6 +195,81 @@ def test_golden_decode_batch(ctx, golden):
         assert S[ost[0]] == v["final_status"], v["name"]
         if v["final_status"] == "Ok":
             assert got.reshape(-1)[: dl[0]].tobytes().hex() == v["data"]
+    ctx.set_decode_path(0)
+
+
+def _sequences(rng, nobj, k, m, L, sparsity, dep_frac):
+    """nobj piece sequences: random coefficient vectors (a fraction zeroed), some pieces replaced by
+    combinations of earlier ones (dependent), random data bytes."""
+    seqs = np.zeros((nobj, m, k + L), np.uint8)
+    for o in range(nobj):
+        for p in range(m):
+            if p >= 2 and rng.random() < dep_frac:
+                a, b = rng.integers(0, p, 2)
+                c = int(rng.integers(0, 256))
+                seqs[o, p] = seqs[o, a] ^ MUL[c][seqs[o, b]]
+            else:
+                cv = rng.integers(0, 256, k, dtype=np.uint8)
+                cv[rng.random(k) < sparsity] = 0
+                seqs[o, p, :k] = cv
+                seqs[o, p, k:] = rng.integers(0, 256, L, dtype=np.uint8)
+    return seqs
+
+
+@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("k,m,L,sparsity,dep", [(8, 14, 5, 0.7, 0.1), (8, 12, 33, 0.9, 0.0), (32, 40, 64, 0.0, 0.2),
+                                                (32, 36, 16, 0.6, 0.1), (17, 30, 7, 0.5, 0.2), (70, 80, 16, 0.3, 0.05),
+                                                (1, 3, 4, 0.5, 0.0), (128, 130, 16, 0.0, 0.02)])
+def test_decode_batch_vs_oracle_sequences(ctx, path, k, m, L, sparsity, dep):
+    """Device (and host) elimination: every decode() status, the rank and the padded payload rows equal the
+    oracle's full-row RREF, for dense, sparse (diagonal-pivot quirk) and dependent pieces."""
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(k * 1000 + m + int(100 * sparsity))
+    nobj = 12
+    seqs = _sequences(rng, nobj, k, m, L, sparsity, dep)
+    decoded = dev(np.zeros((nobj, k, L), np.uint8))
+    ctx.set_decode_path(path)
+    try:
+        pst, ost, dl = batch.decode_batch(dev(seqs), k, decoded, ctx)
+    finally:
+        ctx.set_decode_path(0)
+    got = host(decoded)
+    for o in range(nobj):
+        od = OracleDecoder(L, k)
+        want = [S[od.decode(p)] for p in seqs[o]]
+        assert [S[x] for x in pst[o]] == want, (o, [S[x] for x in pst[o]], want)
+        pay = od.padded_payload()
+        assert np.array_equal(got[o, : pay.shape[0]], pay), o
+        assert not got[o, pay.shape[0]:].any()
+        st, data = od.get_decoded_data()
+        assert S[ost[o]] == S[st], o
+        if st == 0:
+            assert int(dl[o]) == data.size
+
+
+def test_decode_batch_device_async_outputs(ctx, orc):
+    import torch
+
+    from rlnc_amd import batch
+
+    k, L, nobj, m = 32, 4096, 6, 34
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, (nobj, k * L - 1), dtype=np.uint8)
+    src = np.stack([orc.pad(d, k) for d in data])
+    pieces = np.stack([orc.encode(src[o], rng.integers(0, 256, (m, k), dtype=np.uint8)) for o in range(nobj)])
+    decoded = torch.zeros((nobj, k, L), dtype=torch.uint8, device="cuda:0")
+    ps = torch.zeros((nobj, m), dtype=torch.int32, device="cuda:0")
+    os_ = torch.zeros(nobj, dtype=torch.int32, device="cuda:0")
+    dl = torch.zeros(nobj, dtype=torch.int64, device="cuda:0")
+    batch.decode_batch_device(dev(pieces), k, decoded, ps, os_, dl, ctx)
+    torch.cuda.synchronize()
+    for o in range(nobj):
+        od = OracleDecoder(L, k)
+        assert ps[o].cpu().tolist() == [od.decode(p) for p in pieces[o]]
+        if int(os_[o]) == 0:
+            assert int(dl[o]) == data[o].size
+            assert np.array_equal(decoded[o].cpu().numpy().reshape(-1)[: data[o].size], data[o])
 
 
 # ------------------------------------------------------------------------------------------------
