@@ -227,13 +227,14 @@ __device__ int clean_append(const Mat &M, const uint32_t *tab, int r, int k, boo
     __syncthreads();
     if (lane == 0) M.b[r * M.S + r] = 1;
     __syncthreads();
-    for (int w0 = 0; w0 < D; w0 += 64) {
-        const int ww = w0 + w;
-        if (g < G && ww < D) {
-            const uint32_t src = M.w[r * D + ww] & from_mask(ww, r);
-            for (int j = g; j < r; j += G) {
-                const uint32_t q = M.at(j, r);
-                if (q) M.w[j * D + ww] ^= mul4(tab, q, src);
+    // the quotient M[j][r] is read once per row, before any column block of that row is rewritten (the
+    // block holding column r zeroes it)
+    for (int j = g; j < r; j += G) {
+        const uint32_t q = M.at(j, r);
+        if (q) {
+            for (int w0 = 0; w0 < D; w0 += 64) {
+                const int ww = w0 + w;
+                if (ww < D) M.w[j * D + ww] ^= mul4(tab, q, M.w[r * D + ww] & from_mask(ww, r));
             }
         }
     }

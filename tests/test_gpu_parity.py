@@ -219,7 +219,8 @@ def _sequences(rng, nobj, k, m, L, sparsity, dep_frac):
 @pytest.mark.parametrize("path", [1, 2])
 @pytest.mark.parametrize("k,m,L,sparsity,dep", [(8, 14, 5, 0.7, 0.1), (8, 12, 33, 0.9, 0.0), (32, 40, 64, 0.0, 0.2),
                                                 (32, 36, 16, 0.6, 0.1), (17, 30, 7, 0.5, 0.2), (70, 80, 16, 0.3, 0.05),
-                                                (1, 3, 4, 0.5, 0.0), (128, 130, 16, 0.0, 0.02)])
+                                                (1, 3, 4, 0.5, 0.0), (128, 130, 16, 0.0, 0.02),
+                                                (16, 300, 8, 0.2, 0.1), (100, 170, 12, 0.8, 0.1)])
 def test_decode_batch_vs_oracle_sequences(ctx, path, k, m, L, sparsity, dep):
     """Device (and host) elimination: every decode() status, the rank and the padded payload rows equal the
     oracle's full-row RREF, for dense, sparse (diagonal-pivot quirk) and dependent pieces."""
