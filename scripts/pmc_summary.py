@@ -1,29 +1,52 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc CSV output per kernel (mean counter value per dispatch)."""
+"""Summarise rocprofv3 --pmc CSV output: mean counter value per dispatch, grouped by (kernel, grid size).
+
+FETCH_SIZE is reported in KiB and, on gfx950, counts half the bytes of a wide coalesced stream
+(MI355X_MICROARCH.md §HBM); `hbm_read_bytes` below applies that ×2 correction, `hbm_write_bytes` uses
+WRITE_SIZE (KiB, exact for 16-B-per-lane stores).
+"""
 import collections
 import csv
 import glob
+import json
 import os
 import sys
 
-root = sys.argv[1]
-acc = collections.defaultdict(lambda: collections.defaultdict(list))
-durs = collections.defaultdict(list)
-for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
-    for row in csv.DictReader(open(f)):
-        name = row.get("Kernel_Name", "?")
-        short = name.split("(")[0][-60:]
-        acc[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
-for f in glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True):
-    for row in csv.DictReader(open(f)):
-        short = row["Kernel_Name"].split("(")[0][-60:]
-        durs[short].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
-for k, cs in acc.items():
-    if "rlnc" not in k and "gf_" not in k:
-        continue
-    print(k)
-    d = durs.get(k, [])
-    if d:
-        print(f"   duration_ns(mean, profiled) = {sum(d)/len(d):.0f}  n={len(d)}")
-    for c, v in sorted(cs.items()):
-        print(f"   {c:28s} {sum(v)/len(v):.4g}   (n={len(v)})")
+
+def short(name: str) -> str:
+    head = name.rsplit("(", 1)[0] if name.endswith(")") else name
+    return head.replace("(anonymous namespace)::", "")[-90:]
+
+
+def main(root: str):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            key = (short(row["Kernel_Name"]), int(row["Grid_Size"]))
+            acc[key][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            acc[key]["_dur_ns"].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    out = {}
+    for (name, grid), cs in sorted(acc.items()):
+        if "rlnc" not in name:
+            continue
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        d = m.pop("_dur_ns")
+        line = {"kernel": name, "grid": grid, "profiled_ns": round(d)}
+        line.update({c: round(v, 1) for c, v in sorted(m.items())})
+        if "GRBM_GUI_ACTIVE" in m and d:
+            line["clock_GHz_est"] = round(m["GRBM_GUI_ACTIVE"] / 8 / d, 3)
+        if "FETCH_SIZE" in m:
+            line["hbm_read_bytes"] = round(m["FETCH_SIZE"] * 1024 * 2)
+        if "WRITE_SIZE" in m:
+            line["hbm_write_bytes"] = round(m["WRITE_SIZE"] * 1024)
+        if "SQ_WAVE_CYCLES" in m and m["SQ_WAVE_CYCLES"]:
+            for c in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+                if c in m:
+                    line[c + "_frac"] = round(m[c] / m["SQ_WAVE_CYCLES"], 3)
+        out[f"{name}@{grid}"] = line
+        print(json.dumps(line))
+    return out
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
