@@ -99,6 +99,7 @@ typedef struct rlnc_matmul_desc {
 } rlnc_matmul_desc;
 int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc);
 /* Kernel variant for A/B measurement: 0 = perm (3-bit split tables in LDS consumed by v_perm_b32,
+ * 2 = perm3 (three sources per step: 24 bits in eight 3-bit chunks, tables pre-summed across coefficients),
  * default), 1 = nibble (the reference's 4-bit split LOW/HIGH tables looked up from LDS byte-wise).
  * max_tile_rows caps the output rows per workgroup (0 = automatic, else 1/2/4/8/16/32). */
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows);

@@ -167,6 +167,146 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_perm_kernel(MatmulParams p
     }
 }
 
+// Three-source variant: the 24 bits of three source bytes (x, y, z) are cut into eight 3-bit chunks
+//   x0-2 | x3-5 | x6,x7,y0 | y1-3 | y4-6 | y7,z0,z1 | z2-4 | z5-7
+// and each chunk indexes an 8-entry table that already sums the contributions of the coefficients it
+// straddles, so three multiply-accumulates of a word cost 8 v_perm_b32 + 4 v_bitop3_b32 (4.0 VALU ops per
+// word-multiply-add instead of 4.5).  XOR is associative and GF(2^8) products are exact, so the result is
+// byte-identical to the reference's sequential dst ^= c_j · src_j loop.
+constexpr int kKC3 = 33;  // coefficient chunk: 11 triples
+
+__device__ __forceinline__ void triple_tables(uint8_t cx, uint8_t cy, uint8_t cz, uint4 out[4]) {
+    uint8_t b[24];  // basis: b[t] = contribution of bit t of the 24-bit chunk stream
+    uint8_t mx = cx, my = cy, mz = cz;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        b[t] = mx;
+        b[8 + t] = my;
+        b[16 + t] = mz;
+        mx = gf_xtime(mx);
+        my = gf_xtime(my);
+        mz = gf_xtime(mz);
+    }
+    uint32_t w[16];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            uint8_t e = 0;
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+                if (v & (1 << t)) e ^= b[3 * c + t];
+            if (v < 4)
+                lo |= uint32_t(e) << (8 * v);
+            else
+                hi |= uint32_t(e) << (8 * (v - 4));
+        }
+        w[2 * c] = lo;
+        w[2 * c + 1] = hi;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+struct Sel3 {
+    uint32_t s[8][4];
+};
+
+__device__ __forceinline__ Sel3 selectors3(uint4 X, uint4 Y, uint4 Z) {
+    Sel3 r;
+    const uint32_t xs[4] = {X.x, X.y, X.z, X.w}, ys[4] = {Y.x, Y.y, Y.z, Y.w}, zs[4] = {Z.x, Z.y, Z.z, Z.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t x = xs[q], y = ys[q], z = zs[q];
+        r.s[0][q] = x & 0x07070707u;
+        r.s[1][q] = (x >> 3) & 0x07070707u;
+        r.s[2][q] = ((x >> 6) & 0x03030303u) | ((y << 2) & 0x04040404u);
+        r.s[3][q] = (y >> 1) & 0x07070707u;
+        r.s[4][q] = (y >> 4) & 0x07070707u;
+        r.s[5][q] = ((y >> 7) & 0x01010101u) | ((z << 1) & 0x06060606u);
+        r.s[6][q] = (z >> 2) & 0x07070707u;
+        r.s[7][q] = (z >> 5) & 0x07070707u;
+    }
+    return r;
+}
+
+template <int NT, bool ALIGNED>
+__global__ __launch_bounds__(kThreads) void gf_matmul_perm3_kernel(MatmulParams p, int row_tiles, int col_blocks) {
+    constexpr int KT = kKC3 / 3;
+    __shared__ uint4 s_tab[KT][NT][4];
+
+    int rt, cb, obj;
+    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    const int row0 = rt * NT;
+    const int rows_here = min(NT, p.n_out - row0);
+    const int64_t col = int64_t(cb) * kColBlock + int64_t(threadIdx.x) * kBytesPerThread;
+    const int nbytes = col < p.width ? int(min<int64_t>(kBytesPerThread, p.width - col)) : 0;
+    const uint8_t *in_base = p.in + int64_t(obj) * p.in_obj + col;
+    const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
+    const uint4 zero = make_uint4(0, 0, 0, 0);
+
+    uint32_t acc[NT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0u;
+
+    for (int j0 = 0; j0 < p.n_in; j0 += kKC3) {
+        const int kc = min(kKC3, p.n_in - j0);
+        const int kt = (kc + 2) / 3;
+        if (j0) __syncthreads();
+        for (int e = threadIdx.x; e < KT * NT; e += kThreads) {
+            const int i = e % NT, t = e / NT;
+            uint8_t c3[3] = {0, 0, 0};
+            if (i < rows_here)
+                for (int u = 0; u < 3; ++u)
+                    if (3 * t + u < kc) c3[u] = coef_base[int64_t(i) * p.coef_row + j0 + 3 * t + u];
+            triple_tables(c3[0], c3[1], c3[2], s_tab[t][i]);
+        }
+        __syncthreads();
+        if (nbytes > 0) {
+            const uint8_t *rowp = in_base + int64_t(j0) * p.in_row;
+            auto ld = [&](int j) { return j < kc ? load16<ALIGNED>(rowp + int64_t(j) * p.in_row, nbytes) : zero; };
+            uint4 nx = ld(0), ny = ld(1), nz = ld(2);
+            for (int t = 0; t < kt; ++t) {
+                const Sel3 s = selectors3(nx, ny, nz);
+                // prefetch the next triple of source rows while this one is multiplied
+                nx = ld(3 * t + 3);
+                ny = ld(3 * t + 4);
+                nz = ld(3 * t + 5);
+#pragma unroll
+                for (int i = 0; i < NT; ++i) {
+                    const uint4 a = s_tab[t][i][0], b = s_tab[t][i][1], c = s_tab[t][i][2], d = s_tab[t][i][3];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t u0 = xor3(vperm(a.y, a.x, s.s[0][q]), vperm(a.w, a.z, s.s[1][q]),
+                                                 vperm(b.y, b.x, s.s[2][q]));
+                        const uint32_t u1 = xor3(vperm(b.w, b.z, s.s[3][q]), vperm(c.y, c.x, s.s[4][q]),
+                                                 vperm(c.w, c.z, s.s[5][q]));
+                        const uint32_t u2 = xor3(vperm(d.y, d.x, s.s[6][q]), vperm(d.w, d.z, s.s[7][q]), acc[i][q]);
+                        acc[i][q] = xor3(u0, u1, u2);
+                    }
+                }
+            }
+        }
+    }
+
+    if (nbytes > 0) {
+        uint8_t *out_base = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + col;
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+            if (i < rows_here)
+                store16<ALIGNED>(out_base + int64_t(i) * p.out_row,
+                                 make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]), nbytes);
+    }
+    if (p.hdr != nullptr && cb == 0) {
+        uint8_t *h = p.hdr + int64_t(obj) * p.hdr_obj + int64_t(row0) * p.hdr_row;
+        for (int e = threadIdx.x; e < rows_here * p.n_in; e += kThreads) {
+            const int i = e / p.n_in, j = e % p.n_in;
+            h[int64_t(i) * p.hdr_row + j] = coef_base[int64_t(i) * p.coef_row + j];
+        }
+    }
+}
+
 // Ablation baseline: the reference's 4-bit split (LOW/HIGH nibble tables, simd_mul_table.rs:36-80) in
 // LDS, one ds_read_u8 per nibble per byte per lane.
 template <int NT, bool ALIGNED>
@@ -242,7 +382,12 @@ hipError_t launch_nt(const MatmulParams &p, hipStream_t s, MatmulVariant v, bool
     if (total <= 0) return hipSuccess;
     if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
     const dim3 grid{unsigned(total)}, block{unsigned(kThreads)};
-    if (v == MatmulVariant::NibbleLds) {
+    if (v == MatmulVariant::Perm3) {
+        if (aligned)
+            hipLaunchKernelGGL((gf_matmul_perm3_kernel<NT, true>), grid, block, 0, s, p, row_tiles, col_blocks);
+        else
+            hipLaunchKernelGGL((gf_matmul_perm3_kernel<NT, false>), grid, block, 0, s, p, row_tiles, col_blocks);
+    } else if (v == MatmulVariant::NibbleLds) {
         if (aligned)
             hipLaunchKernelGGL((gf_matmul_nibble_kernel<NT, true>), grid, block, 0, s, p, row_tiles, col_blocks);
         else

@@ -55,7 +55,7 @@ def main():
                 else:
                     assert torch.equal(out, ref_enc) and torch.equal(dec, ref_dec), c
     for c in configs:
-        line = {"variant": ["perm", "nibble"][c[0]], "tile_rows": c[1]}
+        line = {"variant": ["perm", "nibble", "perm3"][c[0]], "tile_rows": c[1]}
         for name, ma in (("enc", B * n * k * L), ("dec", B * k * k * L)):
             v = sorted(res[c][name])
             line[name + "_ms_med"] = round(v[len(v) // 2], 4)

@@ -1,0 +1,82 @@
+"""CPU (gloo, world_size 2): the multi-rank path of bench.py — barrier-bracketed timing, max-over-ranks
+elapsed time and summed bytes — with the oracle as the per-rank work (objects sharded, no data-path
+collective).  Runs here without a GPU; the GPU bench uses the same Dist/timed_loop code over RCCL."""
+import os
+import socket
+
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import time
+
+    import numpy as np
+
+    import bench
+    from oracle.oracle import Oracle, OracleDecoder
+
+    d = bench.Dist().init("gloo")
+    orc = Oracle()
+    k, L, n, m, B = 8, 512, 12, 8, 3
+    rng = np.random.default_rng(100 + rank)  # each rank owns different objects
+    src = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    co = rng.integers(0, 256, (B, n, k), dtype=np.uint8)
+    results = []
+
+    def step():
+        out = []
+        for o in range(B):
+            coded = orc.encode(src[o], co[o])
+            dec = OracleDecoder(L, k)
+            for p in coded[:m]:
+                dec.decode(p)
+            out.append(dec.padded_payload())
+        if rank == 1:
+            time.sleep(0.02)  # the slow rank must set the reported time
+        results.append(out)
+
+    el = bench.timed_loop(step, steps=3, warmup=1, dist=d, sync=lambda: None)
+    total = d.allreduce(float(bench.step_bytes(B, k, L, n) * 3), "sum")
+    ok = all(np.array_equal(results[-1][o], src[o]) for o in range(B))
+    q.put((rank, el, total, ok))
+    d.close()
+
+
+def test_two_rank_gloo_timing_and_aggregation():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, el0, tot0, ok0), (r1, el1, tot1, ok1) = res
+    assert ok0 and ok1  # each rank decoded its own objects (full rank with 8 dense pieces of k=8)
+    assert el0 == el1 and el0 >= 3 * 0.02  # max over ranks, the slow rank dominates
+    import bench
+
+    assert tot0 == tot1 == 2 * bench.step_bytes(3, 8, 512, 12) * 3
+
+
+def test_step_bytes_matches_reference_counters():
+    import bench
+
+    k, L = 32, 1 << 20
+    assert bench.encode_counter(k, L) == 34_603_040
+    assert bench.decode_counter(k, L) == 33_555_456
+    assert bench.step_bytes(16, k, L, 64) == 16 * (64 * 34_603_040 + 33_555_456)
