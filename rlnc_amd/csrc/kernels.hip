@@ -93,19 +93,109 @@ __device__ __forceinline__ void decode_block(int total, int row_tiles, int col_b
     obj = rest / col_blocks;
 }
 
-template <int NT, bool ALIGNED>
+// Per-workgroup tile: column block cb of object obj, output rows [row0, row0 + rows_here).
+struct Tile {
+    int row0, rows_here, obj, cb;
+    int64_t col;
+    int nbytes;  // bytes of this lane's 16-byte column slot inside [0, width)
+};
+
+template <int NT>
+__device__ __forceinline__ Tile make_tile(const MatmulParams &p, int row_tiles, int col_blocks) {
+    Tile t;
+    int rt;
+    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, t.cb, t.obj);
+    t.row0 = rt * NT;
+    t.rows_here = min(NT, p.n_out - t.row0);
+    t.col = int64_t(t.cb) * kColBlock + int64_t(threadIdx.x) * kBytesPerThread;
+    t.nbytes = t.col < p.width ? int(min<int64_t>(kBytesPerThread, p.width - t.col)) : 0;
+    return t;
+}
+
+// VEC: plain 16-byte vector access (no per-lane branches in the hot loop, so the prefetched loads stay in
+// flight); otherwise byte-granular access bounded by nbytes (ragged tail / unaligned rows).
+template <bool VEC>
+__device__ __forceinline__ uint4 ld16(const uint8_t *p, int nbytes) {
+    if (VEC) return *reinterpret_cast<const uint4 *>(p);
+    return load16<false>(p, nbytes);
+}
+template <bool VEC>
+__device__ __forceinline__ void st16(uint8_t *p, uint4 v, int nbytes) {
+    if (VEC)
+        *reinterpret_cast<uint4 *>(p) = v;
+    else
+        store16<false>(p, v, nbytes);
+}
+
+template <int NT, bool VEC>
+__device__ __forceinline__ void store_tile(const MatmulParams &p, const Tile &t, const uint32_t (&acc)[NT][4]) {
+    if (!VEC && t.nbytes <= 0) return;
+    uint8_t *out_base = p.out + int64_t(t.obj) * p.out_obj + int64_t(t.row0) * p.out_row + t.col;
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+        if (i < t.rows_here)
+            st16<VEC>(out_base + int64_t(i) * p.out_row, make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]),
+                      t.nbytes);
+}
+
+__device__ __forceinline__ void copy_header(const MatmulParams &p, const Tile &t) {
+    if (p.hdr == nullptr || t.cb != 0) return;
+    const uint8_t *coef_base = p.coef + int64_t(t.obj) * p.coef_obj + int64_t(t.row0) * p.coef_row;
+    uint8_t *h = p.hdr + int64_t(t.obj) * p.hdr_obj + int64_t(t.row0) * p.hdr_row;
+    for (int e = threadIdx.x; e < t.rows_here * p.n_in; e += kThreads) {
+        const int i = e / p.n_in, j = e % p.n_in;
+        h[int64_t(i) * p.hdr_row + j] = coef_base[int64_t(i) * p.coef_row + j];
+    }
+}
+
+// main loop of the 2-source perm kernel over one coefficient chunk (tables already in LDS)
+template <int NT, bool VEC>
+__device__ __forceinline__ void perm_chunk(const MatmulParams &p, const uint8_t *rowp, int kc, int nbytes,
+                                           const uint4 (*s_t01)[NT], const uint32_t (*s_t2)[NT], uint32_t (&acc)[NT][4]) {
+    const uint4 zero = make_uint4(0, 0, 0, 0);
+    uint4 na = ld16<VEC>(rowp, nbytes);
+    uint4 nb = kc > 1 ? ld16<VEC>(rowp + p.in_row, nbytes) : zero;
+    for (int j = 0; j < kc; j += 2) {
+        const uint4 xa = na, xb = nb;
+        // software prefetch of the next row pair while this pair is multiplied
+        if (j + 2 < kc) na = ld16<VEC>(rowp + int64_t(j + 2) * p.in_row, nbytes);
+        nb = (j + 3 < kc) ? ld16<VEC>(rowp + int64_t(j + 3) * p.in_row, nbytes) : zero;
+        const Sel a = selectors(xa);
+        const Sel b = selectors(xb);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+#ifdef RLNC_DIAG_ONE_TABLE
+            // timing-only diagnostic build (wrong output): every row reuses row 0's tables, read once per
+            // row pair from LDS; the empty asm makes each row's copy opaque so no v_perm is CSE'd across rows
+            uint4 ta = s_t01[j][0], tb = s_t01[j + 1][0];
+            uint32_t ta2 = s_t2[j][0], tb2 = s_t2[j + 1][0];
+            asm volatile("" : "+v"(ta.x), "+v"(ta.y), "+v"(ta.z), "+v"(ta.w), "+v"(ta2));
+            asm volatile("" : "+v"(tb.x), "+v"(tb.y), "+v"(tb.z), "+v"(tb.w), "+v"(tb2));
+#else
+            const uint4 ta = s_t01[j][i];
+            const uint32_t ta2 = s_t2[j][i];
+            const uint4 tb = s_t01[j + 1][i];  // zero table when j+1 == kc
+            const uint32_t tb2 = s_t2[j + 1][i];
+#endif
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                uint32_t r = xor3(acc[i][q], vperm(ta.y, ta.x, a.s0[q]), vperm(ta.w, ta.z, a.s1[q]));
+                r = xor3(r, vperm(ta2, ta2, a.s2[q]), vperm(tb.y, tb.x, b.s0[q]));
+                acc[i][q] = xor3(r, vperm(tb.w, tb.z, b.s1[q]), vperm(tb2, tb2, b.s2[q]));
+            }
+        }
+    }
+}
+
+// VEC: every lane owns a full, aligned 16-byte slot (all blocks but a ragged/unaligned tail)
+template <int NT, bool VEC>
 __global__ __launch_bounds__(kThreads) void gf_matmul_perm_kernel(MatmulParams p, int row_tiles, int col_blocks) {
     __shared__ uint4 s_t01[kKC][NT];
     __shared__ uint32_t s_t2[kKC][NT];
 
-    int rt, cb, obj;
-    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
-    const int row0 = rt * NT;
-    const int rows_here = min(NT, p.n_out - row0);
-    const int64_t col = int64_t(cb) * kColBlock + int64_t(threadIdx.x) * kBytesPerThread;
-    const int nbytes = col < p.width ? int(min<int64_t>(kBytesPerThread, p.width - col)) : 0;
-    const uint8_t *in_base = p.in + int64_t(obj) * p.in_obj + col;
-    const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
+    const Tile t = make_tile<NT>(p, row_tiles, col_blocks);
+    const uint8_t *in_base = p.in + int64_t(t.obj) * p.in_obj + t.col;
+    const uint8_t *coef_base = p.coef + int64_t(t.obj) * p.coef_obj + int64_t(t.row0) * p.coef_row;
 
     uint32_t acc[NT][4];
 #pragma unroll
@@ -116,48 +206,100 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_perm_kernel(MatmulParams p
         if (j0) __syncthreads();  // the previous chunk's tables are consumed
         for (int e = threadIdx.x; e < kKC * NT; e += kThreads) {
             const int i = e % NT, j = e / NT;
-            const uint8_t c = (i < rows_here && j < kc) ? coef_base[int64_t(i) * p.coef_row + j0 + j] : uint8_t(0);
-            const PermTable t = make_perm_table(c);
-            s_t01[j][i] = make_uint4(t.t0lo, t.t0hi, t.t1lo, t.t1hi);
-            s_t2[j][i] = t.t2;
+            const uint8_t c = (i < t.rows_here && j < kc) ? coef_base[int64_t(i) * p.coef_row + j0 + j] : uint8_t(0);
+            const PermTable pt = make_perm_table(c);
+            s_t01[j][i] = make_uint4(pt.t0lo, pt.t0hi, pt.t1lo, pt.t1hi);
+            s_t2[j][i] = pt.t2;
         }
         __syncthreads();
-        if (nbytes > 0) {
-            const uint8_t *rowp = in_base + int64_t(j0) * p.in_row;
-            uint4 na = load16<ALIGNED>(rowp, nbytes);
-            uint4 nb = kc > 1 ? load16<ALIGNED>(rowp + p.in_row, nbytes) : make_uint4(0, 0, 0, 0);
-            for (int j = 0; j < kc; j += 2) {
-                const uint4 xa = na, xb = nb;
-                // software prefetch of the next row pair while this pair is multiplied
-                if (j + 2 < kc) na = load16<ALIGNED>(rowp + int64_t(j + 2) * p.in_row, nbytes);
-                nb = (j + 3 < kc) ? load16<ALIGNED>(rowp + int64_t(j + 3) * p.in_row, nbytes) : make_uint4(0, 0, 0, 0);
-                const Sel a = selectors(xa);
-                const Sel b = selectors(xb);
+        if (VEC || t.nbytes > 0)
+            perm_chunk<NT, VEC>(p, in_base + int64_t(j0) * p.in_row, kc, t.nbytes, s_t01, s_t2, acc);
+    }
+    store_tile<NT, VEC>(p, t, acc);
+    copy_header(p, t);
+}
+
+// Wide variant: each lane owns VW 16-byte slots per source row (slot v at column v·4 KiB inside an
+// (VW·4 KiB) block), so every table read from LDS — the measured bottleneck of the VW = 1 kernel (a build
+// that reads one table set per source row ran 2.2× faster) — feeds VW× more multiply-adds.  Full aligned
+// blocks only; ragged tails go to the VW = 1 kernels.
+template <int NT, int VW>
+__global__ __launch_bounds__(kThreads) void gf_matmul_wide_kernel(MatmulParams p, int row_tiles, int col_blocks) {
+    __shared__ uint4 s_t01[kKC][NT];
+    __shared__ uint32_t s_t2[kKC][NT];
+    constexpr int64_t kSlot = int64_t(kThreads) * kBytesPerThread;  // 4 KiB between a lane's slots
+
+    int rt, cb, obj;
+    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    const int row0 = rt * NT;
+    const int rows_here = min(NT, p.n_out - row0);
+    const int64_t col = int64_t(cb) * kSlot * VW + int64_t(threadIdx.x) * kBytesPerThread;
+    const uint8_t *in_base = p.in + int64_t(obj) * p.in_obj + col;
+    const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
+
+    uint32_t acc[NT][VW][4];
 #pragma unroll
-                for (int i = 0; i < NT; ++i) {
-                    const uint4 ta = s_t01[j][i];
-                    const uint32_t ta2 = s_t2[j][i];
-                    const uint4 tb = s_t01[j + 1][i];  // zero table when j+1 == kc
-                    const uint32_t tb2 = s_t2[j + 1][i];
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int v = 0; v < VW; ++v) acc[i][v][0] = acc[i][v][1] = acc[i][v][2] = acc[i][v][3] = 0u;
+
+    for (int j0 = 0; j0 < p.n_in; j0 += kKC) {
+        const int kc = min(kKC, p.n_in - j0);
+        if (j0) __syncthreads();
+        for (int e = threadIdx.x; e < kKC * NT; e += kThreads) {
+            const int i = e % NT, j = e / NT;
+            const uint8_t c = (i < rows_here && j < kc) ? coef_base[int64_t(i) * p.coef_row + j0 + j] : uint8_t(0);
+            const PermTable pt = make_perm_table(c);
+            s_t01[j][i] = make_uint4(pt.t0lo, pt.t0hi, pt.t1lo, pt.t1hi);
+            s_t2[j][i] = pt.t2;
+        }
+        __syncthreads();
+        const uint8_t *rowp = in_base + int64_t(j0) * p.in_row;
+        const uint4 zero = make_uint4(0, 0, 0, 0);
+        uint4 na[VW], nb[VW];
+#pragma unroll
+        for (int v = 0; v < VW; ++v) {
+            na[v] = *reinterpret_cast<const uint4 *>(rowp + v * kSlot);
+            nb[v] = kc > 1 ? *reinterpret_cast<const uint4 *>(rowp + p.in_row + v * kSlot) : zero;
+        }
+        for (int j = 0; j < kc; j += 2) {
+            Sel a[VW], b[VW];
+#pragma unroll
+            for (int v = 0; v < VW; ++v) {
+                a[v] = selectors(na[v]);
+                b[v] = selectors(nb[v]);
+            }
+            // prefetch the next row pair while this pair is multiplied
+#pragma unroll
+            for (int v = 0; v < VW; ++v) {
+                if (j + 2 < kc) na[v] = *reinterpret_cast<const uint4 *>(rowp + int64_t(j + 2) * p.in_row + v * kSlot);
+                nb[v] = (j + 3 < kc) ? *reinterpret_cast<const uint4 *>(rowp + int64_t(j + 3) * p.in_row + v * kSlot) : zero;
+            }
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                const uint4 ta = s_t01[j][i];
+                const uint32_t ta2 = s_t2[j][i];
+                const uint4 tb = s_t01[j + 1][i];
+                const uint32_t tb2 = s_t2[j + 1][i];
+#pragma unroll
+                for (int v = 0; v < VW; ++v)
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        uint32_t r = xor3(acc[i][q], vperm(ta.y, ta.x, a.s0[q]), vperm(ta.w, ta.z, a.s1[q]));
-                        r = xor3(r, vperm(ta2, ta2, a.s2[q]), vperm(tb.y, tb.x, b.s0[q]));
-                        acc[i][q] = xor3(r, vperm(tb.w, tb.z, b.s1[q]), vperm(tb2, tb2, b.s2[q]));
+                        uint32_t r = xor3(acc[i][v][q], vperm(ta.y, ta.x, a[v].s0[q]), vperm(ta.w, ta.z, a[v].s1[q]));
+                        r = xor3(r, vperm(ta2, ta2, a[v].s2[q]), vperm(tb.y, tb.x, b[v].s0[q]));
+                        acc[i][v][q] = xor3(r, vperm(tb.w, tb.z, b[v].s1[q]), vperm(tb2, tb2, b[v].s2[q]));
                     }
-                }
             }
         }
     }
-
-    if (nbytes > 0) {
-        uint8_t *out_base = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + col;
+    uint8_t *out_base = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + col;
 #pragma unroll
-        for (int i = 0; i < NT; ++i)
-            if (i < rows_here)
-                store16<ALIGNED>(out_base + int64_t(i) * p.out_row,
-                                 make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]), nbytes);
-    }
+    for (int i = 0; i < NT; ++i)
+        if (i < rows_here)
+#pragma unroll
+            for (int v = 0; v < VW; ++v)
+                *reinterpret_cast<uint4 *>(out_base + int64_t(i) * p.out_row + v * kSlot) =
+                    make_uint4(acc[i][v][0], acc[i][v][1], acc[i][v][2], acc[i][v][3]);
     if (p.hdr != nullptr && cb == 0) {
         uint8_t *h = p.hdr + int64_t(obj) * p.hdr_obj + int64_t(row0) * p.hdr_row;
         for (int e = threadIdx.x; e < rows_here * p.n_in; e += kThreads) {
@@ -231,20 +373,42 @@ __device__ __forceinline__ Sel3 selectors3(uint4 X, uint4 Y, uint4 Z) {
     return r;
 }
 
-template <int NT, bool ALIGNED>
+template <int NT, bool VEC>
+__device__ __forceinline__ void perm3_chunk(const MatmulParams &p, const uint8_t *rowp, int kc, int nbytes,
+                                            const uint4 (*s_tab)[NT][4], uint32_t (&acc)[NT][4]) {
+    const uint4 zero = make_uint4(0, 0, 0, 0);
+    const int kt = (kc + 2) / 3;
+    auto ld = [&](int j) { return j < kc ? ld16<VEC>(rowp + int64_t(j) * p.in_row, nbytes) : zero; };
+    uint4 nx = ld(0), ny = ld(1), nz = ld(2);
+    for (int t = 0; t < kt; ++t) {
+        const Sel3 s = selectors3(nx, ny, nz);
+        // prefetch the next triple of source rows while this one is multiplied
+        nx = ld(3 * t + 3);
+        ny = ld(3 * t + 4);
+        nz = ld(3 * t + 5);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            const uint4 a = s_tab[t][i][0], b = s_tab[t][i][1], c = s_tab[t][i][2], d = s_tab[t][i][3];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t u0 = xor3(vperm(a.y, a.x, s.s[0][q]), vperm(a.w, a.z, s.s[1][q]), vperm(b.y, b.x, s.s[2][q]));
+                const uint32_t u1 = xor3(vperm(b.w, b.z, s.s[3][q]), vperm(c.y, c.x, s.s[4][q]), vperm(c.w, c.z, s.s[5][q]));
+                const uint32_t u2 = xor3(vperm(d.y, d.x, s.s[6][q]), vperm(d.w, d.z, s.s[7][q]), acc[i][q]);
+                acc[i][q] = xor3(u0, u1, u2);
+            }
+        }
+    }
+}
+
+// VEC: every lane owns a full, aligned 16-byte slot (all blocks but a ragged/unaligned tail)
+template <int NT, bool VEC>
 __global__ __launch_bounds__(kThreads) void gf_matmul_perm3_kernel(MatmulParams p, int row_tiles, int col_blocks) {
     constexpr int KT = kKC3 / 3;
     __shared__ uint4 s_tab[KT][NT][4];
 
-    int rt, cb, obj;
-    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
-    const int row0 = rt * NT;
-    const int rows_here = min(NT, p.n_out - row0);
-    const int64_t col = int64_t(cb) * kColBlock + int64_t(threadIdx.x) * kBytesPerThread;
-    const int nbytes = col < p.width ? int(min<int64_t>(kBytesPerThread, p.width - col)) : 0;
-    const uint8_t *in_base = p.in + int64_t(obj) * p.in_obj + col;
-    const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
-    const uint4 zero = make_uint4(0, 0, 0, 0);
+    const Tile t = make_tile<NT>(p, row_tiles, col_blocks);
+    const uint8_t *in_base = p.in + int64_t(t.obj) * p.in_obj + t.col;
+    const uint8_t *coef_base = p.coef + int64_t(t.obj) * p.coef_obj + int64_t(t.row0) * p.coef_row;
 
     uint32_t acc[NT][4];
 #pragma unroll
@@ -252,59 +416,21 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_perm3_kernel(MatmulParams 
 
     for (int j0 = 0; j0 < p.n_in; j0 += kKC3) {
         const int kc = min(kKC3, p.n_in - j0);
-        const int kt = (kc + 2) / 3;
         if (j0) __syncthreads();
         for (int e = threadIdx.x; e < KT * NT; e += kThreads) {
-            const int i = e % NT, t = e / NT;
+            const int i = e % NT, tt = e / NT;
             uint8_t c3[3] = {0, 0, 0};
-            if (i < rows_here)
+            if (i < t.rows_here)
                 for (int u = 0; u < 3; ++u)
-                    if (3 * t + u < kc) c3[u] = coef_base[int64_t(i) * p.coef_row + j0 + 3 * t + u];
-            triple_tables(c3[0], c3[1], c3[2], s_tab[t][i]);
+                    if (3 * tt + u < kc) c3[u] = coef_base[int64_t(i) * p.coef_row + j0 + 3 * tt + u];
+            triple_tables(c3[0], c3[1], c3[2], s_tab[tt][i]);
         }
         __syncthreads();
-        if (nbytes > 0) {
-            const uint8_t *rowp = in_base + int64_t(j0) * p.in_row;
-            auto ld = [&](int j) { return j < kc ? load16<ALIGNED>(rowp + int64_t(j) * p.in_row, nbytes) : zero; };
-            uint4 nx = ld(0), ny = ld(1), nz = ld(2);
-            for (int t = 0; t < kt; ++t) {
-                const Sel3 s = selectors3(nx, ny, nz);
-                // prefetch the next triple of source rows while this one is multiplied
-                nx = ld(3 * t + 3);
-                ny = ld(3 * t + 4);
-                nz = ld(3 * t + 5);
-#pragma unroll
-                for (int i = 0; i < NT; ++i) {
-                    const uint4 a = s_tab[t][i][0], b = s_tab[t][i][1], c = s_tab[t][i][2], d = s_tab[t][i][3];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const uint32_t u0 = xor3(vperm(a.y, a.x, s.s[0][q]), vperm(a.w, a.z, s.s[1][q]),
-                                                 vperm(b.y, b.x, s.s[2][q]));
-                        const uint32_t u1 = xor3(vperm(b.w, b.z, s.s[3][q]), vperm(c.y, c.x, s.s[4][q]),
-                                                 vperm(c.w, c.z, s.s[5][q]));
-                        const uint32_t u2 = xor3(vperm(d.y, d.x, s.s[6][q]), vperm(d.w, d.z, s.s[7][q]), acc[i][q]);
-                        acc[i][q] = xor3(u0, u1, u2);
-                    }
-                }
-            }
-        }
+        if (VEC || t.nbytes > 0)
+            perm3_chunk<NT, VEC>(p, in_base + int64_t(j0) * p.in_row, kc, t.nbytes, s_tab, acc);
     }
-
-    if (nbytes > 0) {
-        uint8_t *out_base = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + col;
-#pragma unroll
-        for (int i = 0; i < NT; ++i)
-            if (i < rows_here)
-                store16<ALIGNED>(out_base + int64_t(i) * p.out_row,
-                                 make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]), nbytes);
-    }
-    if (p.hdr != nullptr && cb == 0) {
-        uint8_t *h = p.hdr + int64_t(obj) * p.hdr_obj + int64_t(row0) * p.hdr_row;
-        for (int e = threadIdx.x; e < rows_here * p.n_in; e += kThreads) {
-            const int i = e / p.n_in, j = e % p.n_in;
-            h[int64_t(i) * p.hdr_row + j] = coef_base[int64_t(i) * p.coef_row + j];
-        }
-    }
+    store_tile<NT, VEC>(p, t, acc);
+    copy_header(p, t);
 }
 
 // Ablation baseline: the reference's 4-bit split (LOW/HIGH nibble tables, simd_mul_table.rs:36-80) in
@@ -374,31 +500,74 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_nibble_kernel(MatmulParams
     }
 }
 
-template <int NT>
-hipError_t launch_nt(const MatmulParams &p, hipStream_t s, MatmulVariant v, bool aligned) {
+template <int NT, bool VEC>
+hipError_t launch_one(const MatmulParams &p, int64_t width, hipStream_t s, MatmulVariant v) {
     const int row_tiles = (p.n_out + NT - 1) / NT;
-    const int col_blocks = int((p.width + kColBlock - 1) / kColBlock);
+    const int col_blocks = int((width + kColBlock - 1) / kColBlock);
     const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
     if (total <= 0) return hipSuccess;
     if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    MatmulParams q = p;
+    q.width = width;
     const dim3 grid{unsigned(total)}, block{unsigned(kThreads)};
-    if (v == MatmulVariant::Perm3) {
-        if (aligned)
-            hipLaunchKernelGGL((gf_matmul_perm3_kernel<NT, true>), grid, block, 0, s, p, row_tiles, col_blocks);
-        else
-            hipLaunchKernelGGL((gf_matmul_perm3_kernel<NT, false>), grid, block, 0, s, p, row_tiles, col_blocks);
-    } else if (v == MatmulVariant::NibbleLds) {
-        if (aligned)
-            hipLaunchKernelGGL((gf_matmul_nibble_kernel<NT, true>), grid, block, 0, s, p, row_tiles, col_blocks);
-        else
-            hipLaunchKernelGGL((gf_matmul_nibble_kernel<NT, false>), grid, block, 0, s, p, row_tiles, col_blocks);
-    } else {
-        if (aligned)
-            hipLaunchKernelGGL((gf_matmul_perm_kernel<NT, true>), grid, block, 0, s, p, row_tiles, col_blocks);
-        else
-            hipLaunchKernelGGL((gf_matmul_perm_kernel<NT, false>), grid, block, 0, s, p, row_tiles, col_blocks);
-    }
+    if (v == MatmulVariant::Perm3)
+        hipLaunchKernelGGL((gf_matmul_perm3_kernel<NT, VEC>), grid, block, 0, s, q, row_tiles, col_blocks);
+    else if (v == MatmulVariant::NibbleLds)
+        hipLaunchKernelGGL((gf_matmul_nibble_kernel<NT, VEC>), grid, block, 0, s, q, row_tiles, col_blocks);
+    else
+        hipLaunchKernelGGL((gf_matmul_perm_kernel<NT, VEC>), grid, block, 0, s, q, row_tiles, col_blocks);
     return hipGetLastError();
+}
+
+// Aligned operands: whole 4 KiB column blocks go to the branch-free vector kernel, a ragged tail block
+// (width % 4096) to a second launch of the byte-granular kernel.  Unaligned operands: byte kernel only.
+template <int NT>
+hipError_t launch_nt(const MatmulParams &p, hipStream_t s, MatmulVariant v, bool aligned) {
+    if (!aligned) return launch_one<NT, false>(p, p.width, s, v);
+    const int64_t full = (p.width / kColBlock) * kColBlock;
+    if (full > 0) {
+        hipError_t e = launch_one<NT, true>(p, full, s, v);
+        if (e != hipSuccess) return e;
+    }
+    if (full == p.width) return hipSuccess;
+    MatmulParams t = p;
+    t.in = p.in + full;
+    t.out = p.out + full;
+    if (full > 0) t.hdr = nullptr;  // the header rows were written by the first launch
+    return launch_one<NT, false>(t, p.width - full, s, v);
+}
+
+template <int NT, int VW>
+hipError_t launch_wide(const MatmulParams &p, int64_t full, hipStream_t s) {
+    const int row_tiles = (p.n_out + NT - 1) / NT;
+    const int col_blocks = int(full / (int64_t(kColBlock) * VW));
+    const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
+    if (total <= 0) return hipSuccess;
+    if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gf_matmul_wide_kernel<NT, VW>), dim3(unsigned(total)), dim3(kThreads), 0, s, p, row_tiles,
+                       col_blocks);
+    return hipGetLastError();
+}
+
+template <int NT>
+hipError_t launch_nt(const MatmulParams &p, hipStream_t s, MatmulVariant v, bool aligned);
+
+// Wide variant: whole (VW·4 KiB) blocks through gf_matmul_wide_kernel, the rest through the VW = 1 path.
+template <int NT, int VW>
+hipError_t launch_wide_split(const MatmulParams &p, hipStream_t s) {
+    const int64_t blk = int64_t(kColBlock) * VW;
+    const int64_t full = (p.width / blk) * blk;
+    if (full > 0) {
+        hipError_t e = launch_wide<NT, VW>(p, full, s);
+        if (e != hipSuccess) return e;
+    }
+    if (full == p.width) return hipSuccess;
+    MatmulParams t = p;
+    t.in = p.in + full;
+    t.out = p.out + full;
+    t.width = p.width - full;
+    if (full > 0) t.hdr = nullptr;
+    return launch_nt<NT>(t, s, MatmulVariant::Perm, true);
 }
 
 inline bool al16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
@@ -533,6 +702,13 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v) 
     const bool aligned = al16(p.in) && al16(p.out) && al16(p.in_row) && al16(p.out_row) &&
                          (p.n_obj == 1 || (al16(p.in_obj) && al16(p.out_obj)));
     if (p.n_in <= 0) return hipErrorInvalidValue;
+    if (aligned && (v == MatmulVariant::Wide || v == MatmulVariant::Wide4)) {
+        if (v == MatmulVariant::Wide4) return p.n_out <= 4 ? launch_wide_split<4, 4>(p, s) : launch_wide_split<8, 4>(p, s);
+        if (p.n_out <= 4) return launch_wide_split<4, 2>(p, s);
+        if (p.n_out <= 8) return launch_wide_split<8, 2>(p, s);
+        return launch_wide_split<16, 2>(p, s);
+    }
+    if (v == MatmulVariant::Wide || v == MatmulVariant::Wide4) v = MatmulVariant::Perm;
     if (p.n_out <= 1) return launch_nt<1>(p, s, v, aligned);
     if (p.n_out <= 2) return launch_nt<2>(p, s, v, aligned);
     if (p.n_out <= 4) return launch_nt<4>(p, s, v, aligned);

@@ -28,7 +28,7 @@ struct MatmulParams {
     int n_obj;
 };
 
-enum class MatmulVariant : int { Perm = 0, NibbleLds = 1, Perm3 = 2 };
+enum class MatmulVariant : int { Perm = 0, NibbleLds = 1, Perm3 = 2, Wide = 3, Wide4 = 4 };
 
 hipError_t launch_matmul(const MatmulParams &p, hipStream_t stream, MatmulVariant v = MatmulVariant::Perm);
 
