@@ -1,0 +1,225 @@
+// rlnc/full.hpp — C++ mirror of rlnc::full::{Encoder, Decoder, Recoder} and rlnc::RLNCError
+// (itzmeanjan/rlnc 0.8.5, src/full/*.rs, src/common/errors.rs) over the C ABI of librlnc_hip
+// (include/rlnc_hip.h).  Header-only; link with -lrlnc_hip.
+//
+// Names follow the reference; `Encoder::create` stands for `Encoder::new` (a C++ keyword).  Result<T> carries
+// RLNCError like Rust's Result.  Randomness stays with the caller exactly as in the reference: code()/recode()
+// take any Rng with `void fill_bytes(uint8_t *, size_t)` and draw the coefficient bytes on the host
+// (encoder.rs:248, recoder.rs:131).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../rlnc_hip.h"
+
+namespace rlnc {
+
+// errors.rs:3-32, same order (C status = discriminant + 1)
+enum class RLNCError : int {
+    CodingVectorLengthMismatch = 0,
+    DataLengthMismatch,
+    PieceCountZero,
+    DataLengthZero,
+    PieceLengthZero,
+    NotEnoughPiecesToRecode,
+    PieceLengthTooShort,
+    PieceNotUseful,
+    ReceivedAllPieces,
+    NotAllPiecesReceivedYet,
+    InvalidDecodedDataFormat,
+    InvalidPieceLength,
+    InvalidOutputBuffer,
+};
+
+inline const char *to_string(RLNCError e) { return rlnc_status_message(int(e) + 1); }  // errors.rs:34-58
+
+struct DeviceError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+template <class T>
+class Result {
+   public:
+    Result(T v) : ok_(true), v_(std::move(v)) {}
+    Result(RLNCError e) : ok_(false), e_(e) {}
+    bool is_ok() const { return ok_; }
+    bool is_err() const { return !ok_; }
+    RLNCError error() const { return e_; }
+    T &value() {
+        if (!ok_) throw std::logic_error(std::string("unwrap on Err: ") + to_string(e_));
+        return v_;
+    }
+    T unwrap() { return std::move(value()); }
+
+   private:
+    bool ok_;
+    T v_{};
+    RLNCError e_{};
+};
+
+template <>
+class Result<void> {
+   public:
+    Result() : ok_(true) {}
+    Result(RLNCError e) : ok_(false), e_(e) {}
+    bool is_ok() const { return ok_; }
+    bool is_err() const { return !ok_; }
+    RLNCError error() const { return e_; }
+    void unwrap() const {
+        if (!ok_) throw std::logic_error(std::string("unwrap on Err: ") + to_string(e_));
+    }
+
+   private:
+    bool ok_;
+    RLNCError e_{};
+};
+
+namespace detail {
+inline Result<void> status(int s) {
+    if (s == RLNC_OK) return {};
+    if (s >= 1 && s <= 13) return RLNCError(s - 1);
+    throw DeviceError(std::string(rlnc_status_name(s)) + ": " + rlnc_last_error());
+}
+
+// one context per host thread (the reference's &mut self types are single-threaded per object)
+inline rlnc_context *context() {
+    thread_local struct Holder {
+        rlnc_context *c = nullptr;
+        Holder() {
+            const int s = rlnc_context_create(0, &c);
+            if (s != RLNC_OK) throw DeviceError(std::string("rlnc_context_create: ") + rlnc_last_error());
+        }
+        ~Holder() { rlnc_context_destroy(c); }
+    } h;
+    return h.c;
+}
+
+template <class H, void (*Free)(H *)>
+struct Handle {
+    H *h = nullptr;
+    Handle() = default;
+    explicit Handle(H *p) : h(p) {}
+    Handle(Handle &&o) noexcept : h(o.h) { o.h = nullptr; }
+    Handle &operator=(Handle &&o) noexcept {
+        std::swap(h, o.h);
+        return *this;
+    }
+    Handle(const Handle &) = delete;
+    ~Handle() {
+        if (h) Free(h);
+    }
+};
+}  // namespace detail
+
+namespace full {
+
+// encoder.rs:19-270
+class Encoder {
+   public:
+    Encoder() = default;
+    static Result<Encoder> create(const std::vector<uint8_t> &data, size_t piece_count) {  // Encoder::new :85
+        rlnc_encoder *h = nullptr;
+        auto r = detail::status(rlnc_encoder_new(detail::context(), data.data(), data.size(), piece_count, &h));
+        if (r.is_err()) return r.error();
+        return Encoder(h);
+    }
+    size_t get_piece_count() const { return rlnc_encoder_get_piece_count(h_.h); }
+    size_t get_piece_byte_len() const { return rlnc_encoder_get_piece_byte_len(h_.h); }
+    size_t get_full_coded_piece_byte_len() const { return rlnc_encoder_get_full_coded_piece_byte_len(h_.h); }
+    template <class Rng>
+    Result<void> code_with_buf(Rng &rng, std::vector<uint8_t> &full) const {  // encoder.rs:241-250
+        if (full.size() != get_full_coded_piece_byte_len()) return RLNCError::InvalidOutputBuffer;
+        rng.fill_bytes(full.data(), get_piece_count());
+        return detail::status(
+            rlnc_encoder_code_with_buf(h_.h, full.data(), get_piece_count(), full.data(), full.size()));
+    }
+    template <class Rng>
+    std::vector<uint8_t> code(Rng &rng) const {  // encoder.rs:264-269
+        std::vector<uint8_t> v(get_full_coded_piece_byte_len());
+        code_with_buf(rng, v).unwrap();
+        return v;
+    }
+
+   private:
+    explicit Encoder(rlnc_encoder *h) : h_(h) {}
+    detail::Handle<rlnc_encoder, rlnc_encoder_free> h_;
+};
+
+// decoder.rs:9-178
+class Decoder {
+   public:
+    Decoder() = default;
+    static Result<Decoder> create(size_t piece_byte_len, size_t required_piece_count) {  // Decoder::new :65
+        rlnc_decoder *h = nullptr;
+        auto r = detail::status(rlnc_decoder_new(detail::context(), piece_byte_len, required_piece_count, &h));
+        if (r.is_err()) return r.error();
+        return Decoder(h);
+    }
+    Result<void> decode(const std::vector<uint8_t> &piece) {  // decoder.rs:96-118
+        return detail::status(rlnc_decoder_decode(h_.h, piece.data(), piece.size()));
+    }
+    bool is_already_decoded() const { return rlnc_decoder_is_already_decoded(h_.h) != 0; }
+    size_t get_num_pieces_coded_together() const { return rlnc_decoder_get_num_pieces_coded_together(h_.h); }
+    size_t get_piece_byte_len() const { return rlnc_decoder_get_piece_byte_len(h_.h); }
+    size_t get_full_coded_piece_byte_len() const { return rlnc_decoder_get_full_coded_piece_byte_len(h_.h); }
+    size_t get_received_piece_count() const { return rlnc_decoder_get_received_piece_count(h_.h); }
+    size_t get_useful_piece_count() const { return rlnc_decoder_get_useful_piece_count(h_.h); }
+    size_t get_remaining_piece_count() const { return rlnc_decoder_get_remaining_piece_count(h_.h); }
+    Result<std::vector<uint8_t>> get_decoded_data() {  // decoder.rs:136-159
+        std::vector<uint8_t> out(get_num_pieces_coded_together() * get_piece_byte_len());
+        size_t n = 0;
+        auto r = detail::status(rlnc_decoder_get_decoded_data(h_.h, out.data(), out.size(), &n));
+        if (r.is_err()) return r.error();
+        out.resize(n);
+        return out;
+    }
+
+   private:
+    explicit Decoder(rlnc_decoder *h) : h_(h) {}
+    detail::Handle<rlnc_decoder, rlnc_decoder_free> h_;
+};
+
+// recoder.rs:13-172
+class Recoder {
+   public:
+    Recoder() = default;
+    static Result<Recoder> create(const std::vector<uint8_t> &data, size_t full_coded_piece_byte_len,
+                                  size_t num_pieces_coded_together) {  // Recoder::new :68
+        rlnc_recoder *h = nullptr;
+        auto r = detail::status(rlnc_recoder_new(detail::context(), data.data(), data.size(),
+                                                 full_coded_piece_byte_len, num_pieces_coded_together, &h));
+        if (r.is_err()) return r.error();
+        return Recoder(h);
+    }
+    size_t get_original_num_pieces_coded_together() const {
+        return rlnc_recoder_get_original_num_pieces_coded_together(h_.h);
+    }
+    size_t get_num_pieces_recoded_together() const { return rlnc_recoder_get_num_pieces_recoded_together(h_.h); }
+    size_t get_piece_byte_len() const { return rlnc_recoder_get_piece_byte_len(h_.h); }
+    size_t get_full_coded_piece_byte_len() const { return rlnc_recoder_get_full_coded_piece_byte_len(h_.h); }
+    template <class Rng>
+    Result<void> recode_with_buf(Rng &rng, std::vector<uint8_t> &full) {  // recoder.rs:122-153
+        if (full.size() != get_full_coded_piece_byte_len()) return RLNCError::InvalidOutputBuffer;
+        std::vector<uint8_t> r(get_num_pieces_recoded_together());
+        rng.fill_bytes(r.data(), r.size());
+        return detail::status(rlnc_recoder_recode_with_buf(h_.h, r.data(), r.size(), full.data(), full.size()));
+    }
+    template <class Rng>
+    std::vector<uint8_t> recode(Rng &rng) {  // recoder.rs:166-171
+        std::vector<uint8_t> v(get_full_coded_piece_byte_len());
+        recode_with_buf(rng, v).unwrap();
+        return v;
+    }
+
+   private:
+    explicit Recoder(rlnc_recoder *h) : h_(h) {}
+    detail::Handle<rlnc_recoder, rlnc_recoder_free> h_;
+};
+
+}  // namespace full
+}  // namespace rlnc
