@@ -280,7 +280,7 @@ def main():
                         f"first {m} (configs[2]); {B} objects per GPU per step",
             "k": k, "piece_bytes": L, "coded_per_object": n, "decoded_from": m, "objects_per_gpu": B,
             "parallelism": f"objects sharded over {dist.world} rank(s), no data-path collective",
-            "kernel_variant": ["perm", "nibble", "perm3", "wide2", "wide4"][args.variant],
+            "kernel_variant": ["perm", "nibble", "perm3", "wide2", "wide4", "bitsliced"][args.variant],
         },
         "roofline": roofline,
         "cpu_baseline": None,

@@ -105,7 +105,7 @@ struct rlnc_context {
     rlnc::MatmulVariant variant = rlnc::MatmulVariant::Perm;
     int max_tile_rows = 0;
     int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination
-    DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len, ws_pstat, ws_rank;
+    DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len, ws_pstat, ws_rank, ws_idx;
     PinBuf pin_a, pin_b, pin_c;
 
     int activate() const {
@@ -122,11 +122,17 @@ struct rlnc_context {
                 q.coef = p.coef + int64_t(r0) * p.coef_row;
                 q.out = p.out + int64_t(r0) * p.out_row;
                 if (p.hdr) q.hdr = p.hdr + int64_t(r0) * p.hdr_row;
-                HIP_TRY(rlnc::launch_matmul(q, stream, variant));
+                if (int st = launch(q)) return st;
             }
             return RLNC_OK;
         }
-        HIP_TRY(rlnc::launch_matmul(p, stream, variant));
+        return launch(p);
+    }
+    int launch(const rlnc::MatmulParams &p) {
+        const size_t need = rlnc::matmul_scratch_bytes(p, variant);
+        if (need)
+            if (int st = ws_idx.ensure(need)) return st;
+        HIP_TRY(rlnc::launch_matmul(p, stream, variant, ws_idx.p, ws_idx.cap));
         return RLNC_OK;
     }
 };
@@ -323,7 +329,7 @@ int rlnc_set_decode_path(rlnc_context *ctx, int path) {
 
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows) {
     CHECK_ARG(ctx != nullptr);
-    CHECK_ARG(variant >= 0 && variant <= 4);
+    CHECK_ARG(variant >= 0 && variant <= 5);
     CHECK_ARG(max_tile_rows == 0 || max_tile_rows == 1 || max_tile_rows == 2 || max_tile_rows == 4 ||
               max_tile_rows == 8 || max_tile_rows == 16 || max_tile_rows == 32);
     ctx->variant = static_cast<rlnc::MatmulVariant>(variant);

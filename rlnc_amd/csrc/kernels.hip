@@ -574,6 +574,104 @@ inline bool al16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 1
 inline bool al16(int64_t v) { return (v & 15) == 0; }
 
 // ---------------------------------------------------------------------------------------------------
+// Bit-sliced variant (gen_bitslice.py has the full derivation).  Measured on gfx950: v_perm_b32 issues at
+// ~4.1 cycles/wave64, so the 3-perm lookup costs ~19 cycles per 32-bit multiply-add; GF(2^8) multiply by
+// c is instead a GF(2)-linear map on bit-planes, applied with 16 register-indexed XORs per 32 bytes per
+// group, the index pair shared by two groups (s_set_gpr_idx_idx + 2 v_xor_b32, ~2 cycles per XOR), i.e.
+// ~8 cycles of issue per 32 bytes·source·row plus the amortised transposes.
+// ---------------------------------------------------------------------------------------------------
+#include "bitslice_asm.inc"
+
+constexpr int kBsRows = RLNC_BS_NT;           // output rows per workgroup
+constexpr int kBsColBlock = 16384;            // 256 lanes × 64 B
+constexpr int kBsRowDwords = RLNC_BS_ROW_DWORDS;  // packed indices per (row, source)
+
+// Index n = 2·o + h of (row, source) says which of the source's planes 4h..4h+3 feed output plane o: bit b
+// of idx = bit o of (c · 2^(4h+b)).  Packed three per dword as bytes 0x10 | idx, byte 3 = 0x10 (see
+// gen_bitslice.py: the byte above each index supplies M0[15:12], the relative-SRC0 enable).  Stream order
+// [obj][row tile][j][row in tile][6 dwords] is the order the main kernel consumes it; rows past n_out get
+// c = 0 (all indices 0: XOR of the zero register).
+__global__ __launch_bounds__(64) void bs_index_kernel(const uint8_t *coef, int64_t coef_obj, int64_t coef_row,
+                                                      int n_out, int n_in, int row_tiles, uint32_t *stream) {
+    const int j = blockIdx.x, rt = blockIdx.y, obj = blockIdx.z;
+    const int i = threadIdx.x / kBsRowDwords, d = threadIdx.x % kBsRowDwords;
+    if (i >= kBsRows) return;
+    const int row = rt * kBsRows + i;
+    const uint32_t c = row < n_out ? coef[int64_t(obj) * coef_obj + int64_t(row) * coef_row + j] : 0u;
+    uint32_t m[8];  // c · 2^e
+    m[0] = c;
+    for (int e = 1; e < 8; ++e) m[e] = ((m[e - 1] << 1) ^ ((m[e - 1] & 0x80u) ? 0x11Bu : 0u)) & 0xFFu;
+    uint32_t word = 0x10u << 24;
+    for (int b3 = 0; b3 < 3; ++b3) {
+        const int n = 3 * d + b3;
+        uint32_t idx = 0;
+        if (n < 16) {
+            const int o = n >> 1, h = n & 1;
+            for (int b = 0; b < 4; ++b) idx |= ((m[4 * h + b] >> o) & 1u) << b;
+        }
+        word |= (0x10u | idx) << (8 * b3);
+    }
+    stream[((int64_t(obj) * row_tiles + rt) * n_in + j) * (kBsRows * kBsRowDwords) + threadIdx.x] = word;
+}
+
+__global__ __launch_bounds__(kThreads) void gf_matmul_bs_kernel(MatmulParams p, const uint32_t *stream,
+                                                                int row_tiles, int col_blocks) {
+    int rt, cb, obj;
+    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    const int row0 = rt * kBsRows;
+    const int rows = min(kBsRows, p.n_out - row0);
+    if (p.hdr != nullptr && cb == 0) {
+        Tile t;
+        t.obj = obj;
+        t.cb = 0;
+        t.row0 = row0;
+        t.rows_here = rows;
+        copy_header(p, t);
+    }
+    const uint8_t *src = p.in + int64_t(obj) * p.in_obj + int64_t(cb) * kBsColBlock;
+    uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + int64_t(cb) * kBsColBlock;
+    const uint32_t *idx = stream + (int64_t(obj) * row_tiles + rt) * p.n_in * (kBsRows * kBsRowDwords);
+    const uint32_t off = (threadIdx.x >> 6) * 4096u + (threadIdx.x & 63u) * 16u;
+    asm volatile(RLNC_BS_ASM
+                 :
+                 : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),
+                   [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows), [off] "v"(off)
+                 : RLNC_BS_CLOBBER_V, RLNC_BS_CLOBBER_S);
+}
+
+// Full 16 KiB column blocks of aligned operands; the caller sends the rest elsewhere.
+bool bs_eligible(const MatmulParams &p, bool aligned) {
+    return aligned && p.width >= kBsColBlock && p.n_out >= 4 && p.in_row < (int64_t(1) << 32) &&
+           p.out_row < (int64_t(1) << 32);
+}
+
+size_t bs_scratch_bytes(const MatmulParams &p) {
+    const int64_t tiles = (p.n_out + kBsRows - 1) / kBsRows;
+    // + one step: the main loop prefetches one index step past the end of the last tile
+    return size_t(int64_t(p.n_obj) * tiles * p.n_in * kBsRows * kBsRowDwords * 4 + 256);
+}
+
+hipError_t launch_bs(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full) {
+    full = (p.width / kBsColBlock) * kBsColBlock;
+    const int row_tiles = (p.n_out + kBsRows - 1) / kBsRows;
+    const int col_blocks = int(full / kBsColBlock);
+    const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
+    if (scratch == nullptr || scratch_bytes < bs_scratch_bytes(p)) return hipErrorInvalidValue;
+    if (total > 0x7FFFFFFFLL || p.n_in > 65535 || row_tiles > 65535 || p.n_obj > 65535) return hipErrorInvalidValue;
+    uint32_t *stream = static_cast<uint32_t *>(scratch);
+    hipLaunchKernelGGL(bs_index_kernel, dim3(unsigned(p.n_in), unsigned(row_tiles), unsigned(p.n_obj)),
+                       dim3(64), 0, s, p.coef, p.coef_obj, p.coef_row, p.n_out, p.n_in, row_tiles,
+                       stream);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    MatmulParams q = p;
+    q.width = full;
+    hipLaunchKernelGGL(gf_matmul_bs_kernel, dim3(unsigned(total)), dim3(kThreads), 0, s, q, stream, row_tiles,
+                       col_blocks);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------------
 // element-wise primitives (simd/mod.rs:18-119); the scalar early-outs are taken on the host
 // ---------------------------------------------------------------------------------------------------
 template <int OP, bool ALIGNED>  // OP 0: v = c·v   1: d ^= s   2: d ^= c·s
@@ -697,11 +795,34 @@ hipError_t launch_final_data_len_ranked(const uint8_t *data, int64_t obj_stride,
     return hipGetLastError();
 }
 
-hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v) {
+static bool matmul_aligned(const MatmulParams &p) {
+    return al16(p.in) && al16(p.out) && al16(p.in_row) && al16(p.out_row) &&
+           (p.n_obj == 1 || (al16(p.in_obj) && al16(p.out_obj)));
+}
+
+size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v) {
+    if (v != MatmulVariant::BitSliced || p.n_out <= 0 || p.n_in <= 0 || p.n_obj <= 0) return 0;
+    return bs_eligible(p, matmul_aligned(p)) ? bs_scratch_bytes(p) : 0;
+}
+
+hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, void *scratch, size_t scratch_bytes) {
     if (p.n_out <= 0 || p.width <= 0 || p.n_obj <= 0) return hipSuccess;
-    const bool aligned = al16(p.in) && al16(p.out) && al16(p.in_row) && al16(p.out_row) &&
-                         (p.n_obj == 1 || (al16(p.in_obj) && al16(p.out_obj)));
+    const bool aligned = matmul_aligned(p);
     if (p.n_in <= 0) return hipErrorInvalidValue;
+    if (v == MatmulVariant::BitSliced) {
+        v = MatmulVariant::Perm;  // whatever the bit-sliced kernel does not cover
+        if (bs_eligible(p, aligned)) {
+            int64_t full = 0;
+            hipError_t e = launch_bs(p, s, scratch, scratch_bytes, full);
+            if (e != hipSuccess || full == p.width) return e;
+            MatmulParams t = p;
+            t.in = p.in + full;
+            t.out = p.out + full;
+            t.width = p.width - full;
+            t.hdr = nullptr;
+            return launch_matmul(t, s, v);
+        }
+    }
     if (aligned && (v == MatmulVariant::Wide || v == MatmulVariant::Wide4)) {
         if (v == MatmulVariant::Wide4) return p.n_out <= 4 ? launch_wide_split<4, 4>(p, s) : launch_wide_split<8, 4>(p, s);
         if (p.n_out <= 4) return launch_wide_split<4, 2>(p, s);

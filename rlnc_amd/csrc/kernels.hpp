@@ -28,9 +28,14 @@ struct MatmulParams {
     int n_obj;
 };
 
-enum class MatmulVariant : int { Perm = 0, NibbleLds = 1, Perm3 = 2, Wide = 3, Wide4 = 4 };
+enum class MatmulVariant : int { Perm = 0, NibbleLds = 1, Perm3 = 2, Wide = 3, Wide4 = 4, BitSliced = 5 };
 
-hipError_t launch_matmul(const MatmulParams &p, hipStream_t stream, MatmulVariant v = MatmulVariant::Perm);
+// Device scratch the BitSliced variant needs for its coefficient-index stream (0 for the others, and for
+// shapes that variant hands to the perm kernel).  launch_matmul fails with hipErrorInvalidValue when a
+// BitSliced launch gets less.
+size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v);
+hipError_t launch_matmul(const MatmulParams &p, hipStream_t stream, MatmulVariant v = MatmulVariant::Perm,
+                         void *scratch = nullptr, size_t scratch_bytes = 0);
 
 // Element-wise primitives (src/common/simd/mod.rs:18-119) on one device vector.
 hipError_t launch_mul_vec_by_scalar(uint8_t *vec, int64_t len, uint8_t scalar, hipStream_t s);

@@ -40,7 +40,8 @@ def main(root: str):
         if "WRITE_SIZE" in m:
             line["hbm_write_bytes"] = round(m["WRITE_SIZE"] * 1024)
         if "SQ_WAVE_CYCLES" in m and m["SQ_WAVE_CYCLES"]:
-            for c in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+            for c in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA",
+                      "SQ_INST_CYCLES_SALU", "SQ_INST_CYCLES_SMEM", "SQ_INST_LEVEL_SMEM"):
                 if c in m:
                     line[c + "_frac"] = round(m[c] / m["SQ_WAVE_CYCLES"], 3)
         out[f"{name}@{grid}"] = line

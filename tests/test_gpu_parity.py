@@ -66,7 +66,7 @@ SHAPES = [(1, 1, 1, 1), (1, 3, 17, 1), (2, 2, 16, 2), (3, 5, 4095, 1), (4, 32, 4
           (9, 40, 32768, 1)]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("n_out,n_in,W,nobj", SHAPES)
 def test_matmul(ctx, variant, n_out, n_in, W, nobj):
     from rlnc_amd import batch
@@ -86,6 +86,67 @@ def test_matmul(ctx, variant, n_out, n_in, W, nobj):
         ctx.set_kernel_variant(0, 0)
     for o in range(nobj):
         assert np.array_equal(got[o], np_matmul(coef[o], inp[o])), o
+
+
+# the bit-sliced kernel takes whole 16 KiB column blocks of >= 4 output rows (8-row tiles, zero-padded
+# index stream for a partial last tile); shapes around those boundaries, ragged tails to the perm kernel
+BS_SHAPES = [(4, 1, 16384, 1), (5, 2, 16384 + 16, 2), (8, 32, 32768, 1), (9, 31, 16384 * 3 + 4096 + 7, 1),
+             (16, 33, 16384 * 2, 3), (64, 32, 16384 * 2 + 48, 1), (32, 100, 16384, 2), (13, 7, 65536 + 5, 1),
+             (3, 5, 16384, 1)]
+
+
+@pytest.mark.parametrize("n_out,n_in,W,nobj", BS_SHAPES)
+def test_matmul_bitsliced(ctx, n_out, n_in, W, nobj):
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(n_out * 7 + n_in * 3 + W + nobj)
+    coef = rng.integers(0, 256, (nobj, n_out, n_in), dtype=np.uint8)
+    coef[:, 0, :] = 1
+    coef[:, -1, :3] = [0, 2, 0x80][: min(3, n_in)]
+    inp = rng.integers(0, 256, (nobj, n_in, W), dtype=np.uint8)
+    inp[:, 0, :256] = np.arange(256, dtype=np.uint8)  # every byte value against every coefficient row
+    out = dev(np.zeros((nobj, n_out, W), np.uint8))
+    ctx.set_kernel_variant(5, 0)
+    try:
+        batch.matmul(dev(coef), dev(inp), out, ctx)
+        got = host(out)
+    finally:
+        ctx.set_kernel_variant(0, 0)
+    for o in range(nobj):
+        assert np.array_equal(got[o], np_matmul(coef[o], inp[o])), o
+
+
+def test_matmul_bitsliced_strided_with_header(ctx):
+    """Padded row strides and the coded-piece header copy, through the raw C ABI descriptor."""
+    import ctypes as C
+
+    import torch
+
+    from rlnc_amd import _lib
+    from rlnc_amd.errors import check
+
+    rng = np.random.default_rng(5)
+    nobj, n_out, n_in, W, pad = 2, 12, 20, 16384 * 2 + 32, 48
+    hdr_w = n_in
+    coef = rng.integers(0, 256, (nobj, n_out, n_in), dtype=np.uint8)
+    inp = rng.integers(0, 256, (nobj, n_in, W + pad), dtype=np.uint8)
+    pieces = dev(np.zeros((nobj, n_out, 64 + W + pad), np.uint8))  # [header (64 B slot) | data | pad]
+    dcoef, dinp = dev(coef), dev(inp)
+    base = pieces.data_ptr()
+    row = 64 + W + pad
+    d = _lib.MatmulDesc(dinp.data_ptr(), n_in * (W + pad), W + pad, dcoef.data_ptr(), n_out * n_in, n_in,
+                        base + 64, n_out * row, row, base, n_out * row, row, n_out, n_in, W, nobj)
+    ctx.set_kernel_variant(5, 0)
+    try:
+        check(ctx.lib.rlnc_gf256_matmul(ctx.h, C.byref(d)), ctx.lib)
+        torch.cuda.synchronize()
+        got = host(pieces)
+    finally:
+        ctx.set_kernel_variant(0, 0)
+    for o in range(nobj):
+        assert np.array_equal(got[o, :, :hdr_w], coef[o])
+        assert np.array_equal(got[o, :, 64:64 + W], np_matmul(coef[o], inp[o, :, :W]))
+        assert not got[o, :, 64 + W:].any() and not got[o, :, hdr_w:64].any()
 
 
 @pytest.mark.parametrize("tile", [1, 2, 4, 8, 16, 32])
