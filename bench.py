@@ -163,7 +163,7 @@ def main():
     ap.add_argument("--piece-bytes", type=int, default=1 << 20)
     ap.add_argument("--coded", type=int, default=64)
     ap.add_argument("--decode-from", type=int, default=32)
-    ap.add_argument("--variant", type=int, default=0, help="0 perm (v_perm_b32), 1 nibble-LDS")
+    ap.add_argument("--variant", type=int, default=5, help="matmul kernel variant: 5 bitsliced (default), 0 perm, 1 nibble-LDS, 2 perm3, 3/4 wide")
     ap.add_argument("--tile-rows", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

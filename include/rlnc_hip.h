@@ -99,12 +99,12 @@ typedef struct rlnc_matmul_desc {
 } rlnc_matmul_desc;
 int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc);
 /* Kernel variant of the GF(2^8) matmul (all bit-identical; the switch exists for A/B measurement):
- *   0 = perm       3-bit split tables in LDS consumed by v_perm_b32 (default)
+ *   0 = perm       3-bit split tables in LDS consumed by v_perm_b32
  *   1 = nibble     the reference's 4-bit LOW/HIGH tables looked up from LDS byte-wise (ablation)
  *   2 = perm3      three sources per step: 24 bits in eight 3-bit chunks, tables pre-summed
  *   3 = wide2, 4 = wide4   perm with 2 / 4 column slots per lane
- *   5 = bitsliced  bit-plane transpose + register-indexed XOR of plane combinations (full 16 KiB column
- *                  blocks of 16-byte-aligned operands with >= 4 output rows; the rest goes to perm)
+ *   5 = bitsliced  bit-plane transpose + register-indexed XOR of plane combinations (default; full 16 KiB
+ *                  column blocks of 16-byte-aligned operands with >= 4 output rows; the rest goes to perm)
  * max_tile_rows caps the output rows per launch/workgroup (0 = automatic, else 1/2/4/8/16/32). */
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows);
 /* Where rlnc_decode_batch runs the coefficient elimination: 0 = auto (device when it fits LDS, default),

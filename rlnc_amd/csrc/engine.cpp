@@ -102,7 +102,7 @@ struct rlnc_context {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
-    rlnc::MatmulVariant variant = rlnc::MatmulVariant::Perm;
+    rlnc::MatmulVariant variant = rlnc::MatmulVariant::BitSliced;
     int max_tile_rows = 0;
     int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination
     DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len, ws_pstat, ws_rank, ws_idx;

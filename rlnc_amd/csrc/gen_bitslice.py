@@ -40,11 +40,14 @@ def RAW(g, d):  # staging registers of the next source row
 
 TMP0 = 208  # 8 temporaries v208..v215
 V_MASK = (216, 217, 218)  # 0xAAAAAAAA, 0xCCCCCCCC, 0xF0F0F0F0
-S_SRC, S_IDX, S_DST = 32, 34, 36
-S_INROW, S_OUTROW, S_CNT, S_ROWS, S_ZERO, S_T0 = 38, 39, 40, 41, 42, 43
-S_BUF = (44, 68)  # two 24-dword index buffers (4 rows x 6 dwords)
+# SGPRs: s32-s34 are the ABI stack/frame/base pointers (reserved even in a stackless kernel), so the block
+# starts at s36; the compiler keeps its own values (kernel arguments, the asm operands) in s0-s31.
+S_BUF = (36, 60)  # two 24-dword index buffers (4 rows x 6 dwords), 4-aligned for s_load_dwordx16/x8
+S_SRC, S_IDX, S_DST = 84, 86, 88
+S_INROW, S_OUTROW, S_CNT, S_ROWS, S_T0 = 90, 91, 92, 93, 94
+FIRST_SGPR = S_BUF[0]
 LAST_VGPR = V_MASK[2]
-LAST_SGPR = S_BUF[1] + STEP * ROW_DW - 1
+LAST_SGPR = S_T0
 STREAM_ROW_BYTES = ROW_DW * 4
 STREAM_J_BYTES = NT * STREAM_ROW_BYTES
 
@@ -127,7 +130,6 @@ def program():
         f"s_mov_b32 s{S_OUTROW}, %[out_row]",
         f"s_mov_b32 s{S_CNT}, %[n_in]",
         f"s_mov_b32 s{S_ROWS}, %[rows]",
-        f"s_mov_b32 s{S_ZERO}, 0",
         f"v_mov_b32 v{V_MASK[0]}, 0xaaaaaaaa",
         f"v_mov_b32 v{V_MASK[1]}, 0xcccccccc",
         f"v_mov_b32 v{V_MASK[2]}, 0xf0f0f0f0",
@@ -156,7 +158,7 @@ def program():
     for g in range(2):
         for h in range(2):
             combos(g, h, L)
-    L.append(f"s_set_gpr_idx_on s{S_ZERO}, gpr_idx(SRC0)")
+    L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0)")
     nsteps = NT // STEP
     for st in range(nsteps):
         cur, nxt = S_BUF[st & 1], S_BUF[(st + 1) & 1]
@@ -194,7 +196,7 @@ def main():
     lines = program()
     here = os.path.dirname(os.path.abspath(__file__))
     clob_v = ", ".join(f'"v{r}"' for r in range(LAST_VGPR + 1))
-    clob_s = ", ".join(f'"s{r}"' for r in range(S_SRC, LAST_SGPR + 1))
+    clob_s = ", ".join(f'"s{r}"' for r in range(FIRST_SGPR, LAST_SGPR + 1))
     body = "\\n\\t".join(lines)
     with open(os.path.join(here, "bitslice_asm.inc"), "w") as f:
         f.write("// GENERATED by gen_bitslice.py -- do not edit.  Inner program of gf_matmul_bs_kernel (kernels.hip).\n")

@@ -632,11 +632,15 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_bs_kernel(MatmulParams p, 
     uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + int64_t(cb) * kBsColBlock;
     const uint32_t *idx = stream + (int64_t(obj) * row_tiles + rt) * p.n_in * (kBsRows * kBsRowDwords);
     const uint32_t off = (threadIdx.x >> 6) * 4096u + (threadIdx.x & 63u) * 16u;
+    // M0 is clobbered on purpose (it carries the XOR index); nothing else in this kernel uses it
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
     asm volatile(RLNC_BS_ASM
                  :
                  : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),
                    [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows), [off] "v"(off)
                  : RLNC_BS_CLOBBER_V, RLNC_BS_CLOBBER_S);
+#pragma clang diagnostic pop
 }
 
 // Full 16 KiB column blocks of aligned operands; the caller sends the rest elsewhere.

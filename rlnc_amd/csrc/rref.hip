@@ -18,7 +18,9 @@
 //     and normalises row r.  Same products, same XORs, same bytes — computed with all lanes at once.
 //     Leaving the clean state (a zero diagonal after the forward pass: SURVEY.md §0.5) switches to the
 //     generic path, which re-checks cleanliness after every piece.
-// GF products use v_perm_b32 with the 3-bit split tables of all 256 multipliers staged in LDS.
+// GF products use v_perm_b32 with the 3-bit split tables of all 256 multipliers staged in LDS (copied from a
+// compile-time table), and all m piece headers are staged in LDS up front when they fit: the per-piece loop
+// then never waits on HBM.
 #include <hip/hip_runtime.h>
 
 #include "../../include/rlnc_hip.h"
@@ -40,6 +42,60 @@ __host__ __device__ inline int rref_row_dwords(int k, int m) {
 namespace {
 
 constexpr int kTabDw = 8;  // dwords per multiplier: t0lo t0hi t1lo t1hi t2 inv - -
+
+// The 256 × kTabDw table, built at compile time (make_perm_table's layout plus c^-1 = c^254).
+struct RrefTable {
+    uint32_t v[256 * kTabDw];
+};
+constexpr RrefTable build_rref_table() {
+    RrefTable t{};
+    for (int c = 0; c < 256; ++c) {
+        uint8_t m[8] = {};
+        m[0] = uint8_t(c);
+        for (int b = 1; b < 8; ++b) m[b] = gf_xtime(m[b - 1]);
+        uint32_t t0lo = 0, t0hi = 0, t1lo = 0, t1hi = 0, t2 = 0;
+        for (int x = 0; x < 8; ++x) {
+            uint8_t a = 0, h = 0;
+            for (int b = 0; b < 3; ++b)
+                if (x & (1 << b)) {
+                    a = uint8_t(a ^ m[b]);
+                    h = uint8_t(h ^ m[b + 3]);
+                }
+            if (x < 4) {
+                t0lo |= uint32_t(a) << (8 * x);
+                t1lo |= uint32_t(h) << (8 * x);
+            } else {
+                t0hi |= uint32_t(a) << (8 * (x - 4));
+                t1hi |= uint32_t(h) << (8 * (x - 4));
+            }
+        }
+        for (int x = 0; x < 4; ++x) {
+            uint8_t a = 0;
+            for (int b = 0; b < 2; ++b)
+                if (x & (1 << b)) a = uint8_t(a ^ m[b + 6]);
+            t2 |= uint32_t(a) << (8 * x);
+        }
+        uint8_t inv = 1, sq = uint8_t(c);  // c^254 (0 for c = 0)
+        for (int e = 254; e; e >>= 1) {
+            if (e & 1) inv = gf_mul_slow(inv, sq);
+            sq = gf_mul_slow(sq, sq);
+        }
+        uint32_t *e = t.v + c * kTabDw;
+        e[0] = t0lo;
+        e[1] = t0hi;
+        e[2] = t1lo;
+        e[3] = t1hi;
+        e[4] = t2;
+        e[5] = c ? inv : 0u;
+    }
+    return t;
+}
+__device__ const RrefTable kRrefTable = build_rref_table();
+// spot checks against the field (gf256.rs:16-44): identity tables of c = 1, 2^-1 = 0x8D, 3^-1 = 0xF6
+static_assert(build_rref_table().v[1 * kTabDw + 0] == 0x03020100u && build_rref_table().v[1 * kTabDw + 1] == 0x07060504u,
+              "c = 1 low table");
+static_assert(build_rref_table().v[2 * kTabDw + 5] == 0x8Du && build_rref_table().v[3 * kTabDw + 5] == 0xF6u,
+              "inverses");
 
 __device__ __forceinline__ uint32_t mul4(const uint32_t *tab, uint32_t q, uint32_t x) {
     const uint4 t = *reinterpret_cast<const uint4 *>(tab + q * kTabDw);
@@ -179,7 +235,24 @@ __device__ bool is_clean(const Mat &M, int R) {
 }
 
 // Clean-state append of row r (see file header).  Returns the new row count; *stays_clean.
-__device__ int clean_append(const Mat &M, const uint32_t *tab, int r, int k, bool *stays_clean) {
+#ifdef RLNC_RREF_PROFILE
+#define PROF_MARK(i)                                      \
+    do {                                                  \
+        const uint64_t _t = __builtin_amdgcn_s_memtime(); \
+        prof[i] += _t - prof_t;                           \
+        prof_t = _t;                                      \
+    } while (0)
+#define PROF_ARGS , uint64_t *prof, uint64_t &prof_t
+#define PROF_PASS , prof, prof_t
+#else
+#define PROF_MARK(i) \
+    do {             \
+    } while (0)
+#define PROF_ARGS
+#define PROF_PASS
+#endif
+
+__device__ int clean_append(const Mat &M, const uint32_t *tab, int r, int k, bool *stays_clean PROF_ARGS) {
     const int lane = threadIdx.x;
     const int D = M.D;
     const int G = D >= 64 ? 1 : 64 / D;  // lane groups splitting the pivot rows
@@ -188,15 +261,26 @@ __device__ int clean_append(const Mat &M, const uint32_t *tab, int r, int k, boo
     // the original coefficients of row r, kept in the spare row k while row r is rewritten
     for (int ww = lane; ww < D; ww += 64) M.w[k * D + ww] = M.w[r * D + ww];
     __syncthreads();
-    // forward (decoder_matrix.rs:143-162 restricted to the new row): row_r ^= Σ_i M[r][i]·row_i
+    PROF_MARK(1);
+    // forward (decoder_matrix.rs:143-162 restricted to the new row): row_r ^= Σ_i M[r][i]·row_i.
+    // Batches of kU rows per lane group: all quotient, table and data loads of a batch are issued before
+    // any product, so the LDS latencies overlap instead of forming one chain per row.
+    constexpr int kU = 8;
     for (int w0 = 0; w0 < D; w0 += 64) {
         const int ww = w0 + w;
+        const bool act = g < G && ww < D;
         uint32_t acc = 0;
-        if (g < G && ww < D) {
-            for (int i = g; i < r; i += G) {
-                const uint32_t q = M.at(k, i);
-                if (q) acc ^= mul4(tab, q, M.w[i * D + ww]);
+        for (int i0 = g; i0 < r; i0 += kU * G) {
+            uint32_t q[kU], x[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int i = i0 + u * G;
+                const bool in = act && i < r;
+                q[u] = in ? M.at(k, i) : 0u;
+                x[u] = in ? M.w[i * D + ww] : 0u;
             }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) acc ^= mul4(tab, q[u], x[u]);
         }
         if (D < 64) {  // reduce the G partial sums (groups are lane blocks of D)
             for (int sh = D; sh < 64; sh <<= 1) acc ^= __shfl_xor(acc, sh);
@@ -204,6 +288,7 @@ __device__ int clean_append(const Mat &M, const uint32_t *tab, int r, int k, boo
         if (g == 0 && ww < D) M.w[r * D + ww] ^= acc;
         __syncthreads();
     }
+    PROF_MARK(2);
     const uint32_t piv = M.at(r, r);
     if (piv == 0) {
         // the step i = r finds no pivot (no rows below), backward does nothing; the row survives iff a
@@ -227,79 +312,121 @@ __device__ int clean_append(const Mat &M, const uint32_t *tab, int r, int k, boo
     __syncthreads();
     if (lane == 0) M.b[r * M.S + r] = 1;
     __syncthreads();
-    // the quotient M[j][r] is read once per row, before any column block of that row is rewritten (the
-    // block holding column r zeroes it)
-    for (int j = g; j < r; j += G) {
-        const uint32_t q = M.at(j, r);
-        if (q) {
-            for (int w0 = 0; w0 < D; w0 += 64) {
-                const int ww = w0 + w;
-                if (ww < D) M.w[j * D + ww] ^= mul4(tab, q, M.w[r * D + ww] & from_mask(ww, r));
+    PROF_MARK(3);
+    // eliminate column r above row r: the quotient M[j][r] of every row of a batch is read before any
+    // column block of those rows is rewritten (the block holding column r zeroes it); row r's data is
+    // loaded once per column block and shared by all rows
+    for (int j0 = g; j0 < r; j0 += kU * G) {
+        uint32_t q[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int j = j0 + u * G;
+            q[u] = j < r ? M.at(j, r) : 0u;
+        }
+        // (one wave: its LDS reads complete in issue order, so these quotients precede the writes below)
+        for (int w0 = 0; w0 < D; w0 += 64) {
+            const int ww = w0 + w;
+            if (g >= G || ww >= D) continue;
+            const uint32_t xr = M.w[r * D + ww] & from_mask(ww, r);
+            uint32_t y[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int j = j0 + u * G;
+                y[u] = j < r ? M.w[j * D + ww] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int j = j0 + u * G;
+                if (j < r) M.w[j * D + ww] = y[u] ^ mul4(tab, q[u], xr);
             }
         }
     }
     __syncthreads();
+    PROF_MARK(4);
     *stays_clean = true;
     return r + 1;
 }
 
-__global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p) {
+// staged headers: m × k bytes after the matrix (hdr_lds = 1), else read from global memory per piece
+__global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p, int hdr_lds) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;  // 256 × kTabDw dwords
     const int lane = threadIdx.x;
     const int o = blockIdx.x;
     const int k = p.k, m = p.m;
+#ifdef RLNC_RREF_PROFILE  // diagnostic build: statuses become per-piece cycle counts, rank the setup cycles
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
     Mat M;
     M.D = rref_row_dwords(k, m);
     M.S = 4 * M.D;
     M.w = lds + 256 * kTabDw;
     M.b = reinterpret_cast<uint8_t *>(M.w);
+    // per-piece statuses stay in LDS until the end: a global store before each __syncthreads would make
+    // its release fence wait for the store to reach memory, once per piece
+    int32_t *St = reinterpret_cast<int32_t *>(M.b + size_t(k + 1) * M.S);
+    uint8_t *H = reinterpret_cast<uint8_t *>(St + ((m + 3) & ~3));
 
-    for (int c = lane; c < 256; c += 64) {
-        const PermTable t = make_perm_table(uint8_t(c));
-        uint8_t inv = 1, sq = uint8_t(c);  // c^254 = c^-1 (0 for c = 0)
-        for (int e = 254; e; e >>= 1) {
-            if (e & 1) inv = gf_mul_slow(inv, sq);
-            sq = gf_mul_slow(sq, sq);
-        }
-        if (c == 0) inv = 0;
-        uint32_t *e = tab + c * kTabDw;
-        e[0] = t.t0lo;
-        e[1] = t.t0hi;
-        e[2] = t.t1lo;
-        e[3] = t.t1hi;
-        e[4] = t.t2;
-        e[5] = inv;
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(kRrefTable.v);
+        uint4 *dst = reinterpret_cast<uint4 *>(tab);
+        for (int q = lane; q < 256 * kTabDw / 4; q += 64) dst[q] = src[q];
     }
+    const uint8_t *base = p.pieces + int64_t(o) * p.obj_stride;
+    if (hdr_lds)
+        for (int e = lane; e < m * k; e += 64) H[e] = base[int64_t(e / k) * p.piece_stride + e % k];
     for (int w = lane; w < (k + 1) * M.D; w += 64) M.w[w] = 0;
     __syncthreads();
 
-    const uint8_t *base = p.pieces + int64_t(o) * p.obj_stride;
-    int32_t *status = p.status + int64_t(o) * m;
     int rows = 0;
     bool clean = true;
+#ifdef RLNC_RREF_PROFILE
+    const uint64_t t_setup = __builtin_amdgcn_s_memtime();
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t prof_t = t_setup;
+#endif
     for (int pc = 0; pc < m; ++pc) {
         if (rows == k) {  // decoder.rs:97-99
-            if (lane == 0) status[pc] = RLNC_ERR_RECEIVED_ALL_PIECES;  // ReceivedAllPieces
+            if (lane == 0) St[pc] = RLNC_ERR_RECEIVED_ALL_PIECES;  // ReceivedAllPieces
             continue;
         }
         // add_row (decoder_matrix.rs:53-62): [coeffs | unit vector of this piece's slot]
-        const uint8_t *hdr = base + int64_t(pc) * p.piece_stride;
-        for (int c = lane; c < M.S; c += 64) M.b[rows * M.S + c] = c < k ? hdr[c] : uint8_t(c == k + pc);
+        // two explicit branches: a run-time choice of pointer would be a flat access (VMEM latency + waits)
+        if (hdr_lds) {
+            for (int c = lane; c < M.S; c += 64) M.b[rows * M.S + c] = c < k ? H[pc * k + c] : uint8_t(c == k + pc);
+        } else {
+            const uint8_t *hdr = base + int64_t(pc) * p.piece_stride;
+            for (int c = lane; c < M.S; c += 64) M.b[rows * M.S + c] = c < k ? hdr[c] : uint8_t(c == k + pc);
+        }
         __syncthreads();
         const int before = rows;
+        PROF_MARK(0);
         if (clean) {
             bool sc;
-            rows = clean_append(M, tab, rows, k, &sc);
+            rows = clean_append(M, tab, rows, k, &sc PROF_PASS);
             clean = sc;
         } else {
             rows = generic_rref(M, tab, rows + 1, k);
+            PROF_MARK(5);
             clean = is_clean(M, rows);
+            PROF_MARK(6);
         }
-        if (lane == 0) status[pc] = rows == before ? RLNC_ERR_PIECE_NOT_USEFUL : RLNC_OK;  // decoder.rs:112-117
+        if (lane == 0) St[pc] = rows == before ? RLNC_ERR_PIECE_NOT_USEFUL : RLNC_OK;  // decoder.rs:112-117
         __syncthreads();
+        PROF_MARK(7);
     }
+    __syncthreads();
+#ifdef RLNC_RREF_PROFILE  // phases: 0 row init, 1 spare copy, 2 forward, 3 normalise, 4 backward, 5 generic, 6 is_clean, 7 status
+    if (lane == 0)
+        for (int i = 0; i < 8 && i < m; ++i) St[i] = int32_t(prof[i]);
+    __syncthreads();
+#endif
+    for (int pc = lane; pc < m; pc += 64) p.status[int64_t(o) * m + pc] = St[pc];
+#ifdef RLNC_RREF_PROFILE
+    if (lane == 0) p.rank[o] = int32_t(t_setup - t_start);
+#else
     if (lane == 0) p.rank[o] = rows;
+#endif
     uint8_t *T = p.T + int64_t(o) * p.T_obj;
     for (int e = lane; e < k * m; e += 64) {
         const int r = e / m, s = e % m;
@@ -309,12 +436,17 @@ __global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p) {
 
 }  // namespace
 
-size_t rref_lds_bytes(int k, int m) { return 256 * kTabDw * 4 + size_t(k + 1) * 4 * size_t(rref_row_dwords(k, m)); }
+size_t rref_lds_bytes(int k, int m) {
+    return 256 * kTabDw * 4 + size_t(k + 1) * 4 * size_t(rref_row_dwords(k, m)) + 4 * ((size_t(m) + 3) & ~size_t(3));
+}
+static size_t rref_lds_bytes_staged(int k, int m) { return rref_lds_bytes(k, m) + ((size_t(k) * m + 15) & ~size_t(15)); }
 
 hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     if (p.n_obj <= 0) return hipSuccess;
-    const size_t lds = rref_lds_bytes(p.k, p.m);
+    size_t lds = rref_lds_bytes(p.k, p.m);
     if (lds > kRrefMaxLds) return hipErrorInvalidValue;
+    const int hdr_lds = rref_lds_bytes_staged(p.k, p.m) <= kRrefMaxLds ? 1 : 0;
+    if (hdr_lds) lds = rref_lds_bytes_staged(p.k, p.m);
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&gf_rref_batch_kernel),
@@ -322,7 +454,7 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL(gf_rref_batch_kernel, dim3(p.n_obj), dim3(64), lds, s, p);
+    hipLaunchKernelGGL(gf_rref_batch_kernel, dim3(p.n_obj), dim3(64), lds, s, p, hdr_lds);
     return hipGetLastError();
 }
 

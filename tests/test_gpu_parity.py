@@ -12,6 +12,8 @@ from tests.gpu_util import MUL, dev, host, np_matmul
 
 pytestmark = pytest.mark.gpu
 
+DEFAULT_VARIANT = 5  # rlnc_context default (bitsliced, perm for what it does not cover)
+
 S = ["Ok", "CodingVectorLengthMismatch", "DataLengthMismatch", "PieceCountZero", "DataLengthZero",
      "PieceLengthZero", "NotEnoughPiecesToRecode", "PieceLengthTooShort", "PieceNotUseful", "ReceivedAllPieces",
      "NotAllPiecesReceivedYet", "InvalidDecodedDataFormat", "InvalidPieceLength", "InvalidOutputBuffer"]
@@ -26,7 +28,7 @@ def ctx():
 
     c = rlnc_amd.Context(0)
     yield c
-    c.set_kernel_variant(0, 0)
+    c.set_kernel_variant(DEFAULT_VARIANT, 0)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -83,7 +85,7 @@ def test_matmul(ctx, variant, n_out, n_in, W, nobj):
         batch.matmul(dev(coef), dev(inp), out, ctx)
         got = host(out)
     finally:
-        ctx.set_kernel_variant(0, 0)
+        ctx.set_kernel_variant(DEFAULT_VARIANT, 0)
     for o in range(nobj):
         assert np.array_equal(got[o], np_matmul(coef[o], inp[o])), o
 
@@ -111,7 +113,7 @@ def test_matmul_bitsliced(ctx, n_out, n_in, W, nobj):
         batch.matmul(dev(coef), dev(inp), out, ctx)
         got = host(out)
     finally:
-        ctx.set_kernel_variant(0, 0)
+        ctx.set_kernel_variant(DEFAULT_VARIANT, 0)
     for o in range(nobj):
         assert np.array_equal(got[o], np_matmul(coef[o], inp[o])), o
 
@@ -142,7 +144,7 @@ def test_matmul_bitsliced_strided_with_header(ctx):
         torch.cuda.synchronize()
         got = host(pieces)
     finally:
-        ctx.set_kernel_variant(0, 0)
+        ctx.set_kernel_variant(DEFAULT_VARIANT, 0)
     for o in range(nobj):
         assert np.array_equal(got[o, :, :hdr_w], coef[o])
         assert np.array_equal(got[o, :, 64:64 + W], np_matmul(coef[o], inp[o, :, :W]))
@@ -162,7 +164,7 @@ def test_matmul_tile_caps(ctx, tile):
         batch.matmul(dev(coef), dev(inp), out, ctx)
         got = host(out)
     finally:
-        ctx.set_kernel_variant(0, 0)
+        ctx.set_kernel_variant(DEFAULT_VARIANT, 0)
     assert np.array_equal(got[0], np_matmul(coef[0], inp[0]))
 
 
