@@ -9,7 +9,8 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librlnc_hip.so")
+# RLNC_LIB_PATH: diagnostic builds only (scripts/bs_diag.sh); the product is the in-tree library
+LIB_PATH = os.environ.get("RLNC_LIB_PATH") or os.path.join(_HERE, "librlnc_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "rlnc_hip.h")
 
 u8p = C.POINTER(C.c_uint8)

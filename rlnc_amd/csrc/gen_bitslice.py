@@ -92,7 +92,12 @@ def combos(g, h, lines):
     ]
 
 
+DIAG = set()  # diagnostic builds only (scripts/bs_diag.sh): "novm" drops source loads, "nosmem" index reloads
+
+
 def loads(lines):
+    if "novm" in DIAG:
+        return
     for g in range(2):
         for half in range(2):
             q = 2 * g + half
@@ -103,6 +108,8 @@ def loads(lines):
 
 def idx_load(buf, byte_off, lines):
     """24 dwords = one 4-row step of the index stream."""
+    if "nosmem" in DIAG and byte_off:
+        return
     lines.append(f"s_load_dwordx16 s[{buf}:{buf + 15}], s[{S_IDX}:{S_IDX + 1}], {hex(byte_off)}")
     lines.append(f"s_load_dwordx8 s[{buf + 16}:{buf + 23}], s[{S_IDX}:{S_IDX + 1}], {hex(byte_off + 64)}")
 
@@ -142,7 +149,8 @@ def program():
         for h in range(2):
             L.append(f"v_mov_b32 {v(G(g, h, 0))}, 0")
     L.append("1:")  # ---- loop over source rows j
-    L.append("s_waitcnt vmcnt(0)")
+    if "novm" not in DIAG:
+        L.append("s_waitcnt vmcnt(0)")
     for g in range(2):
         outs = [G(g, b // 4, 1 << (b % 4)) for b in range(8)]
         transpose([RAW(g, d) for d in range(8)], outs, L)
@@ -162,7 +170,8 @@ def program():
     nsteps = NT // STEP
     for st in range(nsteps):
         cur, nxt = S_BUF[st & 1], S_BUF[(st + 1) & 1]
-        L.append("s_waitcnt lgkmcnt(0)")
+        if "nosmem" not in DIAG or st == 0:
+            L.append("s_waitcnt lgkmcnt(0)")
         # the next step: this source's next rows, or the next source's first rows (stream is [j][row])
         idx_load(nxt, (st + 1) * STEP * STREAM_ROW_BYTES, L)
         for i in range(st * STEP, (st + 1) * STEP):
@@ -193,12 +202,18 @@ def program():
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "bitslice_asm.inc"))
+    ap.add_argument("--diag", default="", help="comma list: novm, nosmem (timing diagnostics, wrong results)")
+    args = ap.parse_args()
+    DIAG.update(x for x in args.diag.split(",") if x)
     lines = program()
-    here = os.path.dirname(os.path.abspath(__file__))
     clob_v = ", ".join(f'"v{r}"' for r in range(LAST_VGPR + 1))
     clob_s = ", ".join(f'"s{r}"' for r in range(FIRST_SGPR, LAST_SGPR + 1))
     body = "\\n\\t".join(lines)
-    with open(os.path.join(here, "bitslice_asm.inc"), "w") as f:
+    with open(args.out, "w") as f:
         f.write("// GENERATED by gen_bitslice.py -- do not edit.  Inner program of gf_matmul_bs_kernel (kernels.hip).\n")
         f.write(f"// {sum(1 for l in lines if l.startswith('v_'))} VALU, "
                 f"{sum(1 for l in lines if l.startswith('s_'))} SALU/SMEM, "

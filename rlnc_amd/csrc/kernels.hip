@@ -580,7 +580,11 @@ inline bool al16(int64_t v) { return (v & 15) == 0; }
 // group, the index pair shared by two groups (s_set_gpr_idx_idx + 2 v_xor_b32, ~2 cycles per XOR), i.e.
 // ~8 cycles of issue per 32 bytes·source·row plus the amortised transposes.
 // ---------------------------------------------------------------------------------------------------
+#ifdef RLNC_BS_ASM_FILE  // diagnostic builds (scripts/bs_diag.sh) substitute a generated variant
+#include RLNC_BS_ASM_FILE
+#else
 #include "bitslice_asm.inc"
+#endif
 
 constexpr int kBsRows = RLNC_BS_NT;           // output rows per workgroup
 constexpr int kBsColBlock = 16384;            // 256 lanes × 64 B
