@@ -42,6 +42,25 @@ def decode_counter(k: int, L: int) -> int:
     return k * (k + L)
 
 
+VARIANTS = ["perm", "nibble", "perm3", "wide2", "wide4", "bitsliced"]
+KERNELS = {"perm": "gf_matmul_perm_kernel", "nibble": "gf_matmul_nibble_kernel", "perm3": "gf_matmul_perm3_kernel",
+           "wide2": "gf_matmul_wide_kernel", "wide4": "gf_matmul_wide_kernel",
+           "bitsliced": "bs_index_kernel + gf_matmul_bs_kernel"}
+
+
+def pmc_traffic(variant: str, B: int, k: int, L: int, n: int):
+    """HBM bytes per encode launch (read + write) measured by rocprofv3 PMC passes (scripts/pmc_bench.sh ->
+    scripts/pmc_traffic.py -> profiles/pmc_traffic.json, FETCH_SIZE x2 gfx950 correction applied), when the
+    committed measurement is of this variant and shape; else None."""
+    try:
+        rec = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))[variant]
+    except (OSError, KeyError, ValueError):
+        return None, None
+    if (rec["objects"], rec["k"], rec["piece_bytes"], rec["coded"]) != (B, k, L, n):
+        return None, None
+    return rec["hbm_read_bytes"] + rec["hbm_write_bytes"], rec["source"]
+
+
 def step_bytes(objects: int, k: int, L: int, n: int) -> int:
     return objects * (n * encode_counter(k, L) + decode_counter(k, L))
 
@@ -244,14 +263,17 @@ def main():
     enc_compulsory = B * (k * L + n * (k + L))       # source read once + coded pieces written
     achieved = enc_alg / (enc_ms * 1e-3) / 1e9
     ma_per_launch = B * n * k * L                    # GF(2^8) multiply-adds per launch
+    variant = VARIANTS[args.variant]
+    traffic, traffic_src = pmc_traffic(variant, B, k, L, n)
     roofline = {
         "bound": "hbm",
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": None,
-        "kernel": "gf_matmul_perm_kernel<32,true> (encode: 64 coded pieces x 16 objects per launch)",
+        "traffic": traffic,
+        "traffic_source": traffic_src,
+        "kernel": f"{KERNELS[variant]} (encode: {n} coded pieces x {B} objects per launch)",
         "kernel_ms": round(enc_ms, 4),
         "outputs_per_pass": n,
         "compulsory_bytes": enc_compulsory,
@@ -280,7 +302,7 @@ def main():
                         f"first {m} (configs[2]); {B} objects per GPU per step",
             "k": k, "piece_bytes": L, "coded_per_object": n, "decoded_from": m, "objects_per_gpu": B,
             "parallelism": f"objects sharded over {dist.world} rank(s), no data-path collective",
-            "kernel_variant": ["perm", "nibble", "perm3", "wide2", "wide4", "bitsliced"][args.variant],
+            "kernel_variant": variant,
         },
         "roofline": roofline,
         "cpu_baseline": None,

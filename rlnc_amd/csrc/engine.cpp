@@ -104,7 +104,8 @@ struct rlnc_context {
     hipStream_t stream = nullptr;
     rlnc::MatmulVariant variant = rlnc::MatmulVariant::BitSliced;
     int max_tile_rows = 0;
-    int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination
+    int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination,
+                          // 3 device elimination with the clean state on LDS (A/B)
     DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len, ws_pstat, ws_rank, ws_idx;
     PinBuf pin_a, pin_b, pin_c;
 
@@ -322,7 +323,7 @@ int rlnc_context_synchronize(rlnc_context *ctx) {
 }
 
 int rlnc_set_decode_path(rlnc_context *ctx, int path) {
-    CHECK_ARG(ctx != nullptr && path >= 0 && path <= 2);
+    CHECK_ARG(ctx != nullptr && path >= 0 && path <= 3);
     ctx->decode_path = path;
     return RLNC_OK;
 }
@@ -826,6 +827,7 @@ static int decode_batch_device_impl(rlnc_context *ctx, const uint8_t *pieces, si
     rp.T_obj = int64_t(k * m);
     rp.status = pstat_dev;
     rp.rank = rank_dev;
+    rp.lds_only = ctx->decode_path == 3 ? 1 : 0;
     HIP_TRY(rlnc::launch_rref_batch(rp, ctx->stream));
     rlnc::MatmulParams p{};
     p.in = pieces + k;
@@ -952,7 +954,7 @@ int rlnc_decode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t obj_strid
     int st = decode_batch_check(ctx, pieces, obj_stride, k, L, m, nobj, decoded);
     if (st) return st;
     const bool fits = rlnc::rref_lds_bytes(int(k), int(m)) <= rlnc::kRrefMaxLds;
-    if (ctx->decode_path == 2 && !fits)
+    if (ctx->decode_path >= 2 && !fits)
         return set_error(RLNC_ERR_INVALID_ARGUMENT, "device elimination forced but k=%zu, m=%zu exceed LDS", k, m);
     if (!fits || ctx->decode_path == 1)
         return decode_batch_host_impl(ctx, pieces, obj_stride, k, L, m, nobj, decoded, piece_status, object_status,

@@ -43,50 +43,60 @@ namespace {
 
 constexpr int kTabDw = 8;  // dwords per multiplier: t0lo t0hi t1lo t1hi t2 inv - -
 
-// The 256 × kTabDw table, built at compile time (make_perm_table's layout plus c^-1 = c^254).
+// The 512 × kTabDw table, built at compile time: entry c < 256 = make_perm_table's layout of multiplier c plus
+// c^-1 = c^254 in dword 5; entry 256 + c = the layout of c^-1 (0 for c = 0), so that "multiply by the
+// inverse of the pivot" is one table read (the register path's normalisation).
+constexpr int kTabEntries = 512;
 struct RrefTable {
-    uint32_t v[256 * kTabDw];
+    uint32_t v[kTabEntries * kTabDw];
 };
+constexpr void fill_perm_entry(uint32_t *e, uint8_t c) {
+    uint8_t m[8] = {};
+    m[0] = c;
+    for (int b = 1; b < 8; ++b) m[b] = gf_xtime(m[b - 1]);
+    uint32_t t0lo = 0, t0hi = 0, t1lo = 0, t1hi = 0, t2 = 0;
+    for (int x = 0; x < 8; ++x) {
+        uint8_t a = 0, h = 0;
+        for (int b = 0; b < 3; ++b)
+            if (x & (1 << b)) {
+                a = uint8_t(a ^ m[b]);
+                h = uint8_t(h ^ m[b + 3]);
+            }
+        if (x < 4) {
+            t0lo |= uint32_t(a) << (8 * x);
+            t1lo |= uint32_t(h) << (8 * x);
+        } else {
+            t0hi |= uint32_t(a) << (8 * (x - 4));
+            t1hi |= uint32_t(h) << (8 * (x - 4));
+        }
+    }
+    for (int x = 0; x < 4; ++x) {
+        uint8_t a = 0;
+        for (int b = 0; b < 2; ++b)
+            if (x & (1 << b)) a = uint8_t(a ^ m[b + 6]);
+        t2 |= uint32_t(a) << (8 * x);
+    }
+    e[0] = t0lo;
+    e[1] = t0hi;
+    e[2] = t1lo;
+    e[3] = t1hi;
+    e[4] = t2;
+}
 constexpr RrefTable build_rref_table() {
     RrefTable t{};
+    // inverses by the generator-3 logarithm (gf256.rs:16-44, 88-108): c^-1 = 3^(255 - log3 c)
+    uint8_t ex[256] = {}, lg[256] = {};
+    uint8_t x = 1;
+    for (int i = 0; i < 255; ++i) {
+        ex[i] = x;
+        lg[x] = uint8_t(i);
+        x = uint8_t(x ^ gf_xtime(x));  // x·3
+    }
     for (int c = 0; c < 256; ++c) {
-        uint8_t m[8] = {};
-        m[0] = uint8_t(c);
-        for (int b = 1; b < 8; ++b) m[b] = gf_xtime(m[b - 1]);
-        uint32_t t0lo = 0, t0hi = 0, t1lo = 0, t1hi = 0, t2 = 0;
-        for (int x = 0; x < 8; ++x) {
-            uint8_t a = 0, h = 0;
-            for (int b = 0; b < 3; ++b)
-                if (x & (1 << b)) {
-                    a = uint8_t(a ^ m[b]);
-                    h = uint8_t(h ^ m[b + 3]);
-                }
-            if (x < 4) {
-                t0lo |= uint32_t(a) << (8 * x);
-                t1lo |= uint32_t(h) << (8 * x);
-            } else {
-                t0hi |= uint32_t(a) << (8 * (x - 4));
-                t1hi |= uint32_t(h) << (8 * (x - 4));
-            }
-        }
-        for (int x = 0; x < 4; ++x) {
-            uint8_t a = 0;
-            for (int b = 0; b < 2; ++b)
-                if (x & (1 << b)) a = uint8_t(a ^ m[b + 6]);
-            t2 |= uint32_t(a) << (8 * x);
-        }
-        uint8_t inv = 1, sq = uint8_t(c);  // c^254 (0 for c = 0)
-        for (int e = 254; e; e >>= 1) {
-            if (e & 1) inv = gf_mul_slow(inv, sq);
-            sq = gf_mul_slow(sq, sq);
-        }
-        uint32_t *e = t.v + c * kTabDw;
-        e[0] = t0lo;
-        e[1] = t0hi;
-        e[2] = t1lo;
-        e[3] = t1hi;
-        e[4] = t2;
-        e[5] = c ? inv : 0u;
+        const uint8_t inv = c ? ex[(255 - lg[c]) % 255] : uint8_t(0);
+        fill_perm_entry(t.v + c * kTabDw, uint8_t(c));
+        t.v[c * kTabDw + 5] = inv;
+        fill_perm_entry(t.v + (256 + c) * kTabDw, inv);
     }
     return t;
 }
@@ -96,6 +106,7 @@ static_assert(build_rref_table().v[1 * kTabDw + 0] == 0x03020100u && build_rref_
               "c = 1 low table");
 static_assert(build_rref_table().v[2 * kTabDw + 5] == 0x8Du && build_rref_table().v[3 * kTabDw + 5] == 0xF6u,
               "inverses");
+static_assert(build_rref_table().v[(256 + 1) * kTabDw + 0] == 0x03020100u, "1^-1 = 1");
 
 __device__ __forceinline__ uint32_t mul4(const uint32_t *tab, uint32_t q, uint32_t x) {
     const uint4 t = *reinterpret_cast<const uint4 *>(tab + q * kTabDw);
@@ -347,10 +358,195 @@ __device__ int clean_append(const Mat &M, const uint32_t *tab, int r, int k, boo
     return r + 1;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Register-resident clean path (same products as clean_append, without LDS round trips on the matrix).
+// Lane (w, g) = (lane % DP, lane / DP), DP = 64 / G dword slots per row; register t of lane (w, g) holds
+// dword w of row G·t + g.  Rows not yet appended are zero in registers, so products with them are no-ops.
+//   forward  (decoder_matrix.rs:143-162 for the new row r): every lane multiplies its rows i < r by the
+//            ORIGINAL coefficient M[r][i] (read from the LDS copy of the new row) and the G partial sums are
+//            XOR-reduced across lane groups: new row = init ^ Σ_i M[r][i]·row_i;
+//   pivot    M[r][r] == 0: not useful (all k coefficient bytes zero) or kept and the clean state ends
+//            (registers are written back to LDS for the generic path);
+//   normalise from column r+1 (:200-211), byte r := 1;
+//   backward (:179-198) every row j < r ^= M[j][r]·row_r, M[j][r] broadcast from lane (r/4, g).
+// ---------------------------------------------------------------------------------------------------
+template <int G, int RT>
+__device__ void regs_to_lds(const Mat &M, const uint32_t (&v)[RT], int rows) {
+    constexpr int DP = 64 / G;
+    const int w = threadIdx.x % DP, g = threadIdx.x / DP;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+        const int row = G * t + g;
+        if (row < rows && w < M.D) M.w[row * M.D + w] = v[t];
+    }
+    __syncthreads();
+}
+
+template <int G, int RT>
+__device__ void lds_to_regs(const Mat &M, uint32_t (&v)[RT], int rows) {
+    constexpr int DP = 64 / G;
+    const int w = threadIdx.x % DP, g = threadIdx.x / DP;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+        const int row = G * t + g;
+        v[t] = (row < rows && w < M.D) ? M.w[row * M.D + w] : 0u;
+    }
+}
+
+__device__ __forceinline__ uint32_t mul4t(uint4 t, uint32_t t2, uint32_t x) {
+    return __builtin_amdgcn_perm(t.y, t.x, x & 0x07070707u) ^ __builtin_amdgcn_perm(t.w, t.z, (x >> 3) & 0x07070707u) ^
+           __builtin_amdgcn_perm(t2, t2, (x >> 6) & 0x03030303u);
+}
+
+// Forward operands of one piece for the current row count r: this lane's dword of the initial row
+// [coeffs | unit vector of slot pc] and its quotients M[r][i] = coefficient i (i = G·t + g < r); with few
+// rows per lane (RT <= 8) also their tables, so the forward products need no LDS read at all.
+template <int G, int RT>
+struct FwdOps {
+    static constexpr bool kPre = RT <= 8;
+    uint32_t init;
+    uint32_t q[RT];
+    uint4 t4[kPre ? RT : 1];
+    uint32_t t2[kPre ? RT : 1];
+};
+
+template <int G, int RT>
+__device__ __forceinline__ void load_fwd(const Mat &M, const uint32_t *tab, const uint8_t *H, int pc, int r, int k,
+                                         FwdOps<G, RT> &f) {
+    constexpr int DP = 64 / G;
+    const int w = threadIdx.x % DP, g = threadIdx.x / DP;
+    const uint8_t *h = H + pc * k;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+        const int i = G * t + g;
+        f.q[t] = i < r ? uint32_t(h[i]) : 0u;
+    }
+    uint32_t init = 0;
+    if (w < M.D) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int c = 4 * w + b;
+            const uint32_t x = c < k ? uint32_t(h[c]) : uint32_t(c == k + pc);
+            init |= x << (8 * b);
+        }
+    }
+    f.init = init;
+    if constexpr (FwdOps<G, RT>::kPre) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+            f.t4[t] = *reinterpret_cast<const uint4 *>(tab + f.q[t] * kTabDw);
+            f.t2[t] = tab[f.q[t] * kTabDw + 4];
+        }
+    }
+}
+
+// acc ^= Σ_t q[t]·x[t] over chunks of 8 (table reads of a chunk issued together)
+template <int RT>
+__device__ __forceinline__ uint32_t dot_chunked(const uint32_t *tab, const uint32_t (&q)[RT], const uint32_t (&x)[RT]) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int c0 = 0; c0 < RT; c0 += 8) {
+        uint4 t4[8];
+        uint32_t t2[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            t4[u] = *reinterpret_cast<const uint4 *>(tab + q[c0 + u] * kTabDw);
+            t2[u] = tab[q[c0 + u] * kTabDw + 4];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc ^= mul4t(t4[u], t2[u], x[c0 + u]);
+    }
+    return acc;
+}
+
+// Runs pieces pc, pc+1, ... on the registers while the matrix stays a clean RREF (the next piece's forward
+// operands are loaded while the current one finishes).  Returns the next piece index; on leaving the clean
+// state (a kept row with a zero diagonal) the whole matrix is written back to LDS and *clean = false.
+template <int G, int RT>
+__device__ int reg_run(const Mat &M, const uint32_t *tab, uint32_t (&v)[RT], const uint8_t *H, int pc, int m, int k,
+                       int &rows, bool &clean, int32_t *St PROF_ARGS) {
+    constexpr int DP = 64 / G;
+    const int lane = threadIdx.x;
+    const int w = lane % DP, g = lane / DP;
+    const bool wl = w < M.D;
+    uint32_t cm = 0;  // coefficient bytes (< k) of this lane's dword
+    if (wl && 4 * w < k) cm = 4 * w + 4 <= k ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (8 * (4 * w + 4 - k)));
+    FwdOps<G, RT> f;
+    load_fwd<G, RT>(M, tab, H, pc, rows, k, f);
+    for (; pc < m; ++pc) {
+        const int r = rows;
+        if (r == k) {  // decoder.rs:97-99
+            if (lane == 0) St[pc] = RLNC_ERR_RECEIVED_ALL_PIECES;
+            continue;
+        }
+        PROF_MARK(0);
+        // forward: new row = init ^ Σ_{i<r} M[r][i]·row_i
+        uint32_t acc = 0;
+        if constexpr (FwdOps<G, RT>::kPre) {
+#pragma unroll
+            for (int t = 0; t < RT; ++t) acc ^= mul4t(f.t4[t], f.t2[t], v[t]);
+        } else {
+            acc = dot_chunked<RT>(tab, f.q, v);
+        }
+#pragma unroll
+        for (int sh = DP; sh < 64; sh <<= 1) acc ^= __shfl_xor(acc, sh);
+        uint32_t nr = f.init ^ acc;
+        PROF_MARK(2);
+        const int rw = r >> 2, rb = 8 * (r & 3);
+        const uint32_t piv = (__builtin_amdgcn_readlane(nr, rw) >> rb) & 0xFFu;
+        if (piv == 0) {
+            const bool keep = ballot((nr & cm) != 0) != 0;  // remove_zero_rows (:222-244)
+            if (lane == 0) St[pc] = keep ? RLNC_OK : RLNC_ERR_PIECE_NOT_USEFUL;
+            if (keep) {  // the row survives with a zero diagonal: leave the clean state (generic path)
+                regs_to_lds<G, RT>(M, v, r);
+                if (g == 0 && wl) M.w[r * M.D + w] = nr;
+                __syncthreads();
+                rows = r + 1;
+                clean = false;
+                return pc + 1;
+            }
+            if (pc + 1 < m) load_fwd<G, RT>(M, tab, H, pc + 1, r, k, f);
+            continue;
+        }
+        // normalise from column r+1 by the inverse of the pivot (:200-211), byte r := 1
+        const uint4 ti4 = *reinterpret_cast<const uint4 *>(tab + (256 + piv) * kTabDw);
+        const uint32_t ti2 = tab[(256 + piv) * kTabDw + 4];
+        const uint32_t mask = from_mask(w, r + 1);
+        nr = (nr & ~mask) | (mul4t(ti4, ti2, nr) & mask);
+        if (w == rw) nr = (nr & ~(0xFFu << rb)) | (1u << rb);
+        PROF_MARK(3);
+        // backward (:179-198): rows j < r ^= M[j][r]·row_r (absent rows are zero: q = 0, no-op)
+        rows = r + 1;
+#pragma unroll
+        for (int c0 = 0; c0 < RT; c0 += 8) {
+            constexpr int U = RT < 8 ? RT : 8;
+            uint4 b4[U];
+            uint32_t b2[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t qb = (__shfl(v[c0 + u], rw + DP * g) >> rb) & 0xFFu;
+                b4[u] = *reinterpret_cast<const uint4 *>(tab + qb * kTabDw);
+                b2[u] = tab[qb * kTabDw + 4];
+            }
+            if (c0 == 0 && pc + 1 < m) load_fwd<G, RT>(M, tab, H, pc + 1, r + 1, k, f);  // overlaps the products
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[c0 + u] ^= mul4t(b4[u], b2[u], nr);
+        }
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+            if (G * t + g == r) v[t] = nr;
+        if (lane == 0) St[pc] = RLNC_OK;
+        PROF_MARK(4);
+    }
+    return pc;
+}
+
 // staged headers: m × k bytes after the matrix (hdr_lds = 1), else read from global memory per piece
+// G > 0: the clean state runs on registers (reg_run<G, RT>); G = 0: on LDS (clean_append)
+template <int G, int RT>
 __global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p, int hdr_lds) {
     extern __shared__ uint32_t lds[];
-    uint32_t *tab = lds;  // 256 × kTabDw dwords
+    uint32_t *tab = lds;  // kTabEntries × kTabDw dwords
     const int lane = threadIdx.x;
     const int o = blockIdx.x;
     const int k = p.k, m = p.m;
@@ -360,32 +556,58 @@ __global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p, int hdr
     Mat M;
     M.D = rref_row_dwords(k, m);
     M.S = 4 * M.D;
-    M.w = lds + 256 * kTabDw;
+    M.w = lds + kTabEntries * kTabDw;
     M.b = reinterpret_cast<uint8_t *>(M.w);
     // per-piece statuses stay in LDS until the end: a global store before each __syncthreads would make
     // its release fence wait for the store to reach memory, once per piece
     int32_t *St = reinterpret_cast<int32_t *>(M.b + size_t(k + 1) * M.S);
     uint8_t *H = reinterpret_cast<uint8_t *>(St + ((m + 3) & ~3));
 
-    {
+    {  // all loads of the table copy in flight at once (one memory latency, not one per iteration)
+        constexpr int kPer = kTabEntries * kTabDw / 4 / 64;
         const uint4 *src = reinterpret_cast<const uint4 *>(kRrefTable.v);
         uint4 *dst = reinterpret_cast<uint4 *>(tab);
-        for (int q = lane; q < 256 * kTabDw / 4; q += 64) dst[q] = src[q];
+        uint4 t4[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) t4[u] = src[lane + 64 * u];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) dst[lane + 64 * u] = t4[u];
     }
     const uint8_t *base = p.pieces + int64_t(o) * p.obj_stride;
-    if (hdr_lds)
-        for (int e = lane; e < m * k; e += 64) H[e] = base[int64_t(e / k) * p.piece_stride + e % k];
+    if (hdr_lds) {  // 16 independent byte loads in flight per batch
+        for (int e0 = 0; e0 < m * k; e0 += 64 * 16) {
+            uint8_t hb[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int e = e0 + lane + 64 * u;
+                hb[u] = e < m * k ? base[int64_t(e / k) * p.piece_stride + e % k] : uint8_t(0);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (e0 + lane + 64 * u < m * k) H[e0 + lane + 64 * u] = hb[u];
+        }
+    }
     for (int w = lane; w < (k + 1) * M.D; w += 64) M.w[w] = 0;
     __syncthreads();
 
     int rows = 0;
     bool clean = true;
+    uint32_t v[G > 0 ? RT : 1];
+#pragma unroll
+    for (int t = 0; t < (G > 0 ? RT : 1); ++t) v[t] = 0;
 #ifdef RLNC_RREF_PROFILE
     const uint64_t t_setup = __builtin_amdgcn_s_memtime();
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t prof_t = t_setup;
 #endif
     for (int pc = 0; pc < m; ++pc) {
+        if constexpr (G > 0) {
+            if (clean) {
+                pc = reg_run<G, RT>(M, tab, v, H, pc, m, k, rows, clean, St PROF_PASS);
+                __syncthreads();
+                if (pc >= m) break;
+            }
+        }
         if (rows == k) {  // decoder.rs:97-99
             if (lane == 0) St[pc] = RLNC_ERR_RECEIVED_ALL_PIECES;  // ReceivedAllPieces
             continue;
@@ -401,7 +623,7 @@ __global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p, int hdr
         __syncthreads();
         const int before = rows;
         PROF_MARK(0);
-        if (clean) {
+        if (G == 0 && clean) {
             bool sc;
             rows = clean_append(M, tab, rows, k, &sc PROF_PASS);
             clean = sc;
@@ -409,12 +631,16 @@ __global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p, int hdr
             rows = generic_rref(M, tab, rows + 1, k);
             PROF_MARK(5);
             clean = is_clean(M, rows);
+            if constexpr (G > 0)
+                if (clean) lds_to_regs<G, RT>(M, v, rows);
             PROF_MARK(6);
         }
         if (lane == 0) St[pc] = rows == before ? RLNC_ERR_PIECE_NOT_USEFUL : RLNC_OK;  // decoder.rs:112-117
         __syncthreads();
         PROF_MARK(7);
     }
+    if constexpr (G > 0)
+        if (clean) regs_to_lds<G, RT>(M, v, rows);
     __syncthreads();
 #ifdef RLNC_RREF_PROFILE  // phases: 0 row init, 1 spare copy, 2 forward, 3 normalise, 4 backward, 5 generic, 6 is_clean, 7 status
     if (lane == 0)
@@ -437,7 +663,7 @@ __global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p, int hdr
 }  // namespace
 
 size_t rref_lds_bytes(int k, int m) {
-    return 256 * kTabDw * 4 + size_t(k + 1) * 4 * size_t(rref_row_dwords(k, m)) + 4 * ((size_t(m) + 3) & ~size_t(3));
+    return kTabEntries * kTabDw * 4 + size_t(k + 1) * 4 * size_t(rref_row_dwords(k, m)) + 4 * ((size_t(m) + 3) & ~size_t(3));
 }
 static size_t rref_lds_bytes_staged(int k, int m) { return rref_lds_bytes(k, m) + ((size_t(k) * m + 15) & ~size_t(15)); }
 
@@ -447,14 +673,25 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     if (lds > kRrefMaxLds) return hipErrorInvalidValue;
     const int hdr_lds = rref_lds_bytes_staged(p.k, p.m) <= kRrefMaxLds ? 1 : 0;
     if (hdr_lds) lds = rref_lds_bytes_staged(p.k, p.m);
+    // register-resident clean path when the matrix fits: rows <= G·RT, row dwords <= 64 / G
+    const int D = rref_row_dwords(p.k, p.m);
+    auto kern = &gf_rref_batch_kernel<0, 1>;
+    if (!p.lds_only && hdr_lds) {  // the register path reads the staged headers
+        if (D <= 16 && p.k <= 32)
+            kern = &gf_rref_batch_kernel<4, 8>;
+        else if (D <= 32 && p.k <= 64)
+            kern = &gf_rref_batch_kernel<2, 32>;
+    }
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&gf_rref_batch_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, int(kRrefMaxLds));
-        if (e != hipSuccess) return e;
+        for (auto f : {&gf_rref_batch_kernel<0, 1>, &gf_rref_batch_kernel<4, 8>, &gf_rref_batch_kernel<2, 32>}) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(f),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, int(kRrefMaxLds));
+            if (e != hipSuccess) return e;
+        }
         attr_set = true;
     }
-    hipLaunchKernelGGL(gf_rref_batch_kernel, dim3(p.n_obj), dim3(64), lds, s, p, hdr_lds);
+    hipLaunchKernelGGL(kern, dim3(p.n_obj), dim3(64), lds, s, p, hdr_lds);
     return hipGetLastError();
 }
 

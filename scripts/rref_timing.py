@@ -42,7 +42,9 @@ def main():
     dirty[:, 1, :] = 0
     dirty[:, 1, 2] = 5  # reduced by row 0 (column 0 is zero) -> diagonal M[1][1] = 0, column 2 nonzero: kept
     cases["dirty_from_piece_1"] = dirty
-    for name, co in cases.items():
+    paths = [int(x) for x in os.environ.get("RREF_PATHS", "2,3").split(",")]  # 2 registers, 3 LDS clean state
+    for (name, co), path in [(c, p) for c in cases.items() for p in paths]:
+        ctx.set_decode_path(path)
         pieces = torch.empty((B, m, k + L), dtype=torch.uint8, device="cuda")
         batch.encode_batch(src, torch.from_numpy(co).cuda(), pieces, ctx)
         out = torch.empty((B, k, L), dtype=torch.uint8, device="cuda")
@@ -59,7 +61,7 @@ def main():
             if r >= 2:
                 times.append(e0.elapsed_time(e1))
         times.sort()
-        line = {"case": name, "decode_ms_med": round(times[len(times) // 2], 4), "decode_ms_min": round(times[0], 4)}
+        line = {"case": name, "decode_path": path, "decode_ms_med": round(times[len(times) // 2], 4), "decode_ms_min": round(times[0], 4)}
         if os.environ.get("RLNC_RREF_PROFILE"):  # diagnostic library: cycles per piece / setup (object 0..2)
             line["phase_cycles_obj0_1"] = pst[:2, :8].cpu().tolist()
             line["phase_names"] = "row_init spare_copy forward normalise backward generic is_clean status"
