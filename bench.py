@@ -42,10 +42,11 @@ def decode_counter(k: int, L: int) -> int:
     return k * (k + L)
 
 
-VARIANTS = ["perm", "nibble", "perm3", "wide2", "wide4", "bitsliced"]
+VARIANTS = ["perm", "nibble", "perm3", "wide2", "wide4", "bitsliced", "bitsliced-jump"]
 KERNELS = {"perm": "gf_matmul_perm_kernel", "nibble": "gf_matmul_nibble_kernel", "perm3": "gf_matmul_perm3_kernel",
            "wide2": "gf_matmul_wide_kernel", "wide4": "gf_matmul_wide_kernel",
-           "bitsliced": "bs_index_kernel + gf_matmul_bs_kernel"}
+           "bitsliced": "bs_index_kernel + gf_matmul_bs_kernel",
+           "bitsliced-jump": "bsj_offset_kernel + gf_matmul_bsj_kernel"}
 
 
 def pmc_traffic(variant: str, B: int, k: int, L: int, n: int):
@@ -182,7 +183,7 @@ def main():
     ap.add_argument("--piece-bytes", type=int, default=1 << 20)
     ap.add_argument("--coded", type=int, default=64)
     ap.add_argument("--decode-from", type=int, default=32)
-    ap.add_argument("--variant", type=int, default=5, help="matmul kernel variant: 5 bitsliced (default), 0 perm, 1 nibble-LDS, 2 perm3, 3/4 wide")
+    ap.add_argument("--variant", type=int, default=6, help="matmul kernel variant: 6 bit-sliced, one code block per coefficient (default), 5 bit-sliced relative XOR, 0 perm, 1 nibble-LDS, 2 perm3, 3/4 wide")
     ap.add_argument("--tile-rows", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -103,8 +103,10 @@ int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc);
  *   1 = nibble     the reference's 4-bit LOW/HIGH tables looked up from LDS byte-wise (ablation)
  *   2 = perm3      three sources per step: 24 bits in eight 3-bit chunks, tables pre-summed
  *   3 = wide2, 4 = wide4   perm with 2 / 4 column slots per lane
- *   5 = bitsliced  bit-plane transpose + register-indexed XOR of plane combinations (default; full 16 KiB
- *                  column blocks of 16-byte-aligned operands with >= 4 output rows; the rest goes to perm)
+ *   5 = bitsliced  bit-plane transpose + register-indexed XOR of plane combinations (full 16 KiB column
+ *                  blocks of 16-byte-aligned operands with >= 4 output rows; the rest goes to perm)
+ *   6 = bitsliced-jump  as 5, but each (row, source) is one call into a code block specialised for the
+ *                  coefficient (16 v_bitop3_b32 XOR3s of plane combinations) -- the default
  * max_tile_rows caps the output rows per launch/workgroup (0 = automatic, else 1/2/4/8/16/32). */
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows);
 /* Where rlnc_decode_batch runs the coefficient elimination: 0 = auto (device when it fits LDS, default),

@@ -50,9 +50,10 @@ class Context:
         """0 auto, 1 host elimination, 2 device elimination (both exact)."""
         check(self.lib.rlnc_set_decode_path(self.h, int(path)), self.lib)
 
-    def set_kernel_variant(self, variant: int = 5, max_tile_rows: int = 0):
-        """GF(2^8) matmul variant (include/rlnc_hip.h): 5 = bitsliced (default), 0 = perm, 1 = nibble (the
-        reference's 4-bit tables, ablation), 2 = perm3, 3/4 = wide2/wide4.  All are bit-identical."""
+    def set_kernel_variant(self, variant: int = 6, max_tile_rows: int = 0):
+        """GF(2^8) matmul variant (include/rlnc_hip.h): 6 = bit-sliced, one code block per coefficient
+        (default), 5 = bit-sliced with register-indexed XORs, 0 = perm, 1 = nibble (the reference's 4-bit
+        tables, ablation), 2 = perm3, 3/4 = wide2/wide4.  All are bit-identical."""
         check(self.lib.rlnc_set_kernel_variant(self.h, int(variant), int(max_tile_rows)), self.lib)
 
 

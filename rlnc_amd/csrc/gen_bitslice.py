@@ -35,18 +35,19 @@ def ACC(i, g, p):  # output row i, group g, plane/dword p
 def G(g, h, v):  # combination v of half h of group g
     return 128 + g * 32 + h * 16 + v
 
-def RAW(g, d):  # staging registers of the next source row
-    return 192 + g * 8 + d
+def RAW(g, d, buf=0):  # staging registers: two buffers, source rows j+1 and j+2 in flight
+    return (192 if buf == 0 else 220) + g * 8 + d
 
 TMP0 = 208  # 8 temporaries v208..v215
 V_MASK = (216, 217, 218)  # 0xAAAAAAAA, 0xCCCCCCCC, 0xF0F0F0F0
+
 # SGPRs: s32-s34 are the ABI stack/frame/base pointers (reserved even in a stackless kernel), so the block
 # starts at s36; the compiler keeps its own values (kernel arguments, the asm operands) in s0-s31.
 S_BUF = (36, 60)  # two 24-dword index buffers (4 rows x 6 dwords), 4-aligned for s_load_dwordx16/x8
 S_SRC, S_IDX, S_DST = 84, 86, 88
 S_INROW, S_OUTROW, S_CNT, S_ROWS, S_T0 = 90, 91, 92, 93, 94
 FIRST_SGPR = S_BUF[0]
-LAST_VGPR = V_MASK[2]
+LAST_VGPR = RAW(1, 7, 1)
 LAST_SGPR = S_T0
 STREAM_ROW_BYTES = ROW_DW * 4
 STREAM_J_BYTES = NT * STREAM_ROW_BYTES
@@ -54,6 +55,10 @@ STREAM_J_BYTES = NT * STREAM_ROW_BYTES
 
 def v(n):
     return f"v{n}"
+
+
+def bank(r):
+    return r % 4
 
 
 def transpose(regs_in, regs_out, lines):
@@ -76,32 +81,23 @@ def transpose(regs_in, regs_out, lines):
 
 
 def combos(g, h, lines):
+    """G[v] for the 11 composite v from the 4 planes (entries 1, 2, 4, 8): one VOP2 XOR each."""
     b = lambda x: v(G(g, h, x))
-    lines += [
-        f"v_xor_b32 {b(3)}, {b(1)}, {b(2)}",
-        f"v_xor_b32 {b(5)}, {b(1)}, {b(4)}",
-        f"v_xor_b32 {b(6)}, {b(2)}, {b(4)}",
-        f"v_bitop3_b32 {b(7)}, {b(1)}, {b(2)}, {b(4)} bitop3:0x96",
-        f"v_xor_b32 {b(9)}, {b(1)}, {b(8)}",
-        f"v_xor_b32 {b(10)}, {b(2)}, {b(8)}",
-        f"v_bitop3_b32 {b(11)}, {b(1)}, {b(2)}, {b(8)} bitop3:0x96",
-        f"v_xor_b32 {b(12)}, {b(4)}, {b(8)}",
-        f"v_bitop3_b32 {b(13)}, {b(1)}, {b(4)}, {b(8)} bitop3:0x96",
-        f"v_bitop3_b32 {b(14)}, {b(2)}, {b(4)}, {b(8)} bitop3:0x96",
-        f"v_xor_b32 {b(15)}, {b(3)}, {b(12)}",
-    ]
+    lines += [f"v_xor_b32 {b(x)}, {b(y)}, {b(z)}" for x, y, z in
+              [(3, 1, 2), (5, 1, 4), (6, 2, 4), (7, 3, 4), (9, 1, 8), (10, 2, 8), (11, 3, 8), (12, 4, 8), (13, 5, 8),
+               (14, 6, 8), (15, 7, 8)]]
 
 
 DIAG = set()  # diagnostic builds only (scripts/bs_diag.sh): "novm" drops source loads, "nosmem" index reloads
 
 
-def loads(lines):
+def loads(lines, buf=0):
     if "novm" in DIAG:
         return
     for g in range(2):
         for half in range(2):
             q = 2 * g + half
-            r0 = RAW(g, 4 * half)
+            r0 = RAW(g, 4 * half, buf)
             off = f" offset:{q * 1024}" if q else ""
             lines.append(f"global_load_dwordx4 v[{r0}:{r0 + 3}], %[off], s[{S_SRC}:{S_SRC + 1}]{off}")
 
@@ -116,15 +112,62 @@ def idx_load(buf, byte_off, lines):
 
 def row_update(i, buf, lines):
     """acc[i] ^= M_c . planes for both groups: 16 M0 writes, 32 relative XORs."""
-    for o in range(8):
-        for h in range(2):
+    # (h, o) order: the two updates of one accumulator are 24 instructions apart, not 3 (dependent VALU
+    # issue); "oh" keeps the old (o, h) order for A/B
+    order = [(o, h) for o in range(8) for h in range(2)] if "oh" in DIAG else [(o, h) for h in range(2) for o in range(8)]
+    for o, h in order:
             n = 2 * o + h
             reg = buf + ROW_DW * (i % STEP) + n // 3
             sh = 8 * (n % 3)
-            lines.append(f"s_mov_b32 m0, s{reg}" if sh == 0 else f"s_lshr_b32 m0, s{reg}, {sh}")
+            if "plainxor" not in DIAG and "nom0" not in DIAG:
+                lines.append(f"s_mov_b32 m0, s{reg}" if sh == 0 else f"s_lshr_b32 m0, s{reg}, {sh}")
             for g in range(2):
                 a = ACC(i, g, o)
-                lines.append(f"v_xor_b32 v{a}, v{G(g, h, 0) - 16}, v{a}")
+                if "plainxor" in DIAG:  # timing only: a fixed combination, no GPR-index mode
+                    lines.append(f"v_xor_b32 v{a}, v{G(g, h, 1 + (n % 15))}, v{a}")
+                else:
+                    lines.append(f"v_xor_b32 v{a}, v{G(g, h, 0) - 16}, v{a}")
+
+
+def body(L, buf):
+    """One source row: its planes come from staging buffer `buf` (loaded two rows earlier), which is then
+    refilled with row j+2 (the last row again past the end: no branch, always in bounds)."""
+    if "novm" not in DIAG:
+        L.append("s_waitcnt vmcnt(4)")  # the other buffer's 4 loads (issued later) may stay in flight
+    for g in range(2):
+        outs = [G(g, b // 4, 1 << (b % 4)) for b in range(8)]
+        if "notrans" in DIAG:  # timing only: planes = raw dwords
+            L += [f"v_mov_b32 v{o}, v{RAW(g, d, buf)}" for d, o in enumerate(outs)]
+        else:
+            transpose([RAW(g, d, buf) for d in range(8)], outs, L)
+    L += [
+        f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1",
+        f"s_cmp_gt_u32 s{S_CNT}, 1",  # row j+2 exists
+        f"s_cselect_b32 s{S_T0}, s{S_INROW}, 0",
+        f"s_add_u32 s{S_SRC}, s{S_SRC}, s{S_T0}",
+        f"s_addc_u32 s{S_SRC + 1}, s{S_SRC + 1}, 0",
+    ]
+    loads(L, buf)
+    for g in range(2):
+        for h in range(2):
+            if "nocombo" not in DIAG:
+                combos(g, h, L)
+    if "plainxor" not in DIAG:
+        L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0)")
+    nsteps = NT // STEP
+    for st in range(nsteps):
+        cur, nxt = S_BUF[st & 1], S_BUF[(st + 1) & 1]
+        if "nosmem" not in DIAG or st == 0:
+            L.append("s_waitcnt lgkmcnt(0)")
+        # the next step: this source's next rows, or the next source's first rows (stream is [j][row])
+        idx_load(nxt, (st + 1) * STEP * STREAM_ROW_BYTES, L)
+        for i in range(st * STEP, (st + 1) * STEP):
+            row_update(i, cur, L)
+    L += [
+        "s_set_gpr_idx_off" if "plainxor" not in DIAG else "s_nop 0",
+        f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
+        f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
+    ]
 
 
 def program():
@@ -141,49 +184,27 @@ def program():
         f"v_mov_b32 v{V_MASK[1]}, 0xcccccccc",
         f"v_mov_b32 v{V_MASK[2]}, 0xf0f0f0f0",
     ]
-    loads(L)
+    # prologue: source rows 0 and 1 in flight (row 0 again when n_in == 1)
+    loads(L, 0)
+    L += [
+        f"s_cmp_gt_u32 s{S_CNT}, 1",
+        f"s_cselect_b32 s{S_T0}, s{S_INROW}, 0",
+        f"s_add_u32 s{S_SRC}, s{S_SRC}, s{S_T0}",
+        f"s_addc_u32 s{S_SRC + 1}, s{S_SRC + 1}, 0",
+    ]
+    loads(L, 1)
     idx_load(S_BUF[0], 0, L)
     for r in range(128):
         L.append(f"v_mov_b32 v{r}, 0")
     for g in range(2):
         for h in range(2):
             L.append(f"v_mov_b32 {v(G(g, h, 0))}, 0")
-    L.append("1:")  # ---- loop over source rows j
-    if "novm" not in DIAG:
-        L.append("s_waitcnt vmcnt(0)")
-    for g in range(2):
-        outs = [G(g, b // 4, 1 << (b % 4)) for b in range(8)]
-        transpose([RAW(g, d) for d in range(8)], outs, L)
-    # next source row (the last iteration re-reads the current one: no branch, always in bounds)
-    L += [
-        f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1",
-        f"s_cmp_eq_u32 s{S_CNT}, 0",
-        f"s_cselect_b32 s{S_T0}, 0, s{S_INROW}",
-        f"s_add_u32 s{S_SRC}, s{S_SRC}, s{S_T0}",
-        f"s_addc_u32 s{S_SRC + 1}, s{S_SRC + 1}, 0",
-    ]
-    loads(L)
-    for g in range(2):
-        for h in range(2):
-            combos(g, h, L)
-    L.append("s_set_gpr_idx_on 0, gpr_idx(SRC0)")
-    nsteps = NT // STEP
-    for st in range(nsteps):
-        cur, nxt = S_BUF[st & 1], S_BUF[(st + 1) & 1]
-        if "nosmem" not in DIAG or st == 0:
-            L.append("s_waitcnt lgkmcnt(0)")
-        # the next step: this source's next rows, or the next source's first rows (stream is [j][row])
-        idx_load(nxt, (st + 1) * STEP * STREAM_ROW_BYTES, L)
-        for i in range(st * STEP, (st + 1) * STEP):
-            row_update(i, cur, L)
-    L += [
-        "s_set_gpr_idx_off",
-        f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
-        f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
-        f"s_cmp_eq_u32 s{S_CNT}, 0",
-        "s_cbranch_scc0 1b",
-        "s_waitcnt vmcnt(0) lgkmcnt(0)",
-    ]
+    # loop over source rows j, two per trip (staging buffers alternate); S_CNT = rows not yet consumed
+    L.append("1:")
+    body(L, 0)
+    L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f"]
+    body(L, 1)
+    L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc0 1b", "3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
     # ---- epilogue: transpose back and store the rows that exist
     for i in range(NT):
         L += [f"s_cmp_gt_u32 s{S_ROWS}, {i}", "s_cbranch_scc0 2f"]
@@ -206,7 +227,7 @@ def main():
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "bitslice_asm.inc"))
-    ap.add_argument("--diag", default="", help="comma list: novm, nosmem (timing diagnostics, wrong results)")
+    ap.add_argument("--diag", default="", help="comma list: novm, nosmem (timing diagnostics, wrong results), nobanks (A/B)")
     args = ap.parse_args()
     DIAG.update(x for x in args.diag.split(",") if x)
     lines = program()

@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""Generate bitslice_jump.inc: the gfx950 inner program of gf_matmul_bsj_kernel (kernels.hip), the bit-sliced
+GF(2^8) matmul whose per-(row, source) work is ONE call into a code block specialised for the coefficient.
+
+Why: on gfx950 (scripts/ubench_ops.hip, profiles/r01_ubench_ops.jsonl) every GPR-index-relative VALU
+instruction issues at ~4.4 cycles per wave64, whatever its form, while v_xor_b32 / v_bitop3_b32 with absolute
+operands issue at ~2.3.  gf_matmul_bs_kernel spends 32 relative XORs + 16 M0 writes per (row, source);
+here the coefficient c selects one of 256 straight-line blocks (s_swappc_b64 / s_setpc_b64) holding the 16
+products of that c as v_bitop3_b32 XOR3s whose combination operands are absolute registers baked into the
+block, only the accumulator (DST and SRC2) relative to the row slot (M0 = 0xC000 | 16 * row).  One call
+costs ~105 cycles at 2 waves/SIMD (scripts/ubench_jump.hip) against ~165 for the relative-XOR form.
+
+Algorithm (one workgroup = 8 output rows x 16 KiB of columns; one lane = 64 bytes as two 32-byte groups):
+  * bit-slicing: a group's 8 dwords (32 bytes) are transposed into 8 bit-planes (plane b = bit b of each
+    of the 32 bytes) by three delta-swap stages; 64-bit shifts move two registers per instruction and the
+    bit-field merges are v_bitop3_b32 (full rate; v_bfi_b32 and 32-bit shifts issue at quarter rate);
+  * for source row j, G[h][v] = XOR of planes {4h + b : bit b of v} (v = 0..15, h = low/high half);
+  * multiply-add by c: acc[o] ^= G[0][lo(c, o)] ^ G[1][hi(c, o)], bit b of lo(c, o) = bit o of c * 2^b and
+    bit b of hi(c, o) = bit o of c * 2^(4 + b) (GF(2)-linearity of x -> c * x) -- block c holds these 16
+    XOR3s for both groups;
+  * the block offsets c * BLOCK_BYTES of all (row, source) pairs come from the prep kernel's stream
+    (s_load_dwordx8 per source, one source ahead); source rows are loaded two ahead into two staging buffers;
+  * after all sources, the accumulators are transposed back and stored.
+Run `python3 gen_bsjump.py` after editing; the output is committed.
+"""
+import argparse
+import os
+
+NT = 8  # output rows per workgroup
+BLOCK_BYTES = 16 * 8 + 4  # 16 VOP3 (8 bytes) + s_setpc_b64 (4 bytes)
+STREAM_J_BYTES = NT * 4  # one dword (block offset) per row
+
+
+# ---- register map ---------------------------------------------------------------------------------------
+def ACC(i, g, p):  # output row i, group g, plane p (the blocks name row 0; M0 adds 16 * i)
+    return i * 16 + g * 8 + p
+
+
+def G(g, h, v):  # combination v of half h of group g (G[g][h][0] = 0)
+    return 128 + g * 32 + h * 16 + v
+
+
+def RAW(g, d, buf):  # staging registers: source rows j+1 and j+2 in flight
+    return 192 + 16 * buf + g * 8 + d
+
+
+TMP0 = 224  # 8 temporaries v224..v231 (4 pairs for 64-bit shifts)
+V_X = 232  # 8 registers v232..v239: the transposes' middle stage / the epilogue's store buffer
+V_MASK = (240, 241, 242)  # 0xAAAAAAAA, 0xCCCCCCCC, 0xF0F0F0F0
+LAST_VGPR = 242
+S_OFF = (36, 44)  # two 8-dword block-offset buffers (4-aligned for s_load_dwordx8)
+S_SRC, S_IDX, S_DST, S_BASE, S_TGT, S_RET = 52, 54, 56, 58, 60, 62
+S_INROW, S_OUTROW, S_CNT, S_ROWS, S_T0 = 64, 65, 66, 67, 68
+FIRST_SGPR, LAST_SGPR = S_OFF[0], S_T0
+BFI = "0xca"  # v_bitop3_b32 truth table of S0 ? S1 : S2 (index = S0 S1 S2)
+
+DIAG = set()
+
+
+def v(n):
+    return f"v{n}"
+
+
+# ---- bit transpose --------------------------------------------------------------------------------------
+# The delta-swap stage k exchanges bit k of the register index with bit k of the bit position (s = 2^k):
+#   a' = (a & ~m) | ((b << s) & m),  b' = (b & m) | ((a >> s) & ~m)   for pairs (a, b = a + s), m = MASK[k].
+# The three stages act on disjoint index bits, so they commute; all three are involutions, hence so is the
+# transpose.  A 64-bit shift of a register pair is exact here: the bits that cross the dword boundary land in
+# the low s bits (left shift) or the high s bits (right shift) of the other dword, which m (resp. ~m)
+# clears -- provided both registers of the pair need the same shift, i.e. have the same bit k.  Stages 1 and
+# 2 find such pairs adjacent in the natural order (stage 1: (2,3), (6,7) left, (0,1), (4,5) right; stage 2:
+# (4,5), (6,7) left, (0,1), (2,3) right); stage 0 runs last, on the order PHYS0 written by stage 2
+# (pairs (1,3), (5,7) left, (0,2), (4,6) right).  Every stage writes a register set disjoint from the one
+# it reads: natural src -> X -> src registers in PHYS0 order -> dst.
+PHYS0 = [0, 2, 1, 3, 4, 6, 5, 7]  # physical slot d holds logical register PHYS0[d]
+SHIFT_PAIRS = {0: ([(1, 3), (5, 7)], [(0, 2), (4, 6)]), 1: ([(2, 3), (6, 7)], [(0, 1), (4, 5)]),
+               2: ([(4, 5), (6, 7)], [(0, 1), (2, 3)])}
+
+
+def stage(k, cur, out, lines):
+    s = 1 << k
+    left, right = SHIFT_PAIRS[k]
+    shl, shr = {}, {}
+    t = TMP0
+    for pairs, op, dst in ((left, "v_lshlrev_b64", shl), (right, "v_lshrrev_b64", shr)):
+        for x, y in pairs:
+            assert cur[y] == cur[x] + 1 and cur[x] % 2 == 0, (k, x, y, cur)
+            lines.append(f"{op} v[{t}:{t + 1}], {s}, v[{cur[x]}:{cur[y]}]")
+            dst[x], dst[y] = t, t + 1
+            t += 2
+    assert not set(cur.values()) & set(out.values())
+    for a in range(8):
+        if (a >> k) & 1:
+            continue
+        b = a + s
+        lines.append(f"v_bitop3_b32 {v(out[a])}, v{V_MASK[k]}, v{shl[b]}, {v(cur[a])} bitop3:{BFI}")  # m ? b<<s : a
+        lines.append(f"v_bitop3_b32 {v(out[b])}, v{V_MASK[k]}, {v(cur[b])}, v{shr[a]} bitop3:{BFI}")  # m ? b : a>>s
+
+
+def transpose(src, dst, lines):
+    """src: natural order (logical r in src[r], aligned consecutive registers); dst: any layout, disjoint
+    from src and X."""
+    X = {r: V_X + r for r in range(8)}
+    regs = [src[r] for r in range(8)]
+    mid = {PHYS0[d]: regs[d] for d in range(8)}
+    stage(1, src, X, lines)
+    stage(2, X, mid, lines)
+    stage(0, mid, dst, lines)
+
+
+def combos(g, h, lines):
+    """G[v] for the 11 composite v from the 4 planes (entries 1, 2, 4, 8): one VOP2 XOR each."""
+    b = lambda x: v(G(g, h, x))
+    lines += [f"v_xor_b32 {b(x)}, {b(y)}, {b(z)}" for x, y, z in
+              [(3, 1, 2), (5, 1, 4), (6, 2, 4), (7, 3, 4), (9, 1, 8), (10, 2, 8), (11, 3, 8), (12, 4, 8), (13, 5, 8),
+               (14, 6, 8), (15, 7, 8)]]
+
+
+# ---- GF(2^8) (0x11B) for the block tables ---------------------------------------------------------------
+def xtime(a):
+    a <<= 1
+    return (a ^ 0x11B) & 0xFF if a & 0x100 else a
+
+
+def block_indices(c):
+    """lo[o], hi[o]: bit b of lo[o] = bit o of c * 2^b, of hi[o] = bit o of c * 2^(4 + b)."""
+    m = [c]
+    for _ in range(7):
+        m.append(xtime(m[-1]))
+    lo = [sum(((m[b] >> o) & 1) << b for b in range(4)) for o in range(8)]
+    hi = [sum(((m[4 + b] >> o) & 1) << b for b in range(4)) for o in range(8)]
+    return lo, hi
+
+
+def blocks(lines):
+    for c in range(256):
+        lo, hi = block_indices(c)
+        for g in range(2):
+            for o in range(8):
+                a = ACC(0, g, o)
+                lines.append(f"v_bitop3_b32 v{a}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])}, v{a} bitop3:0x96")
+        lines.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+
+
+# ---- main program ---------------------------------------------------------------------------------------
+def loads(lines, buf):
+    """Source row j+2 into staging buffer `buf` (memory dword d of group g -> RAW(g, d, buf))."""
+    if "novm" in DIAG:
+        return
+    for g in range(2):
+        for half in range(2):
+            q = 2 * g + half
+            r0 = RAW(g, 4 * half, buf)
+            off = f" offset:{q * 1024}" if q else ""
+            lines.append(f"global_load_dwordx4 v[{r0}:{r0 + 3}], %[off], s[{S_SRC}:{S_SRC + 1}]{off}")
+
+
+def body(L, buf):
+    if "novm" not in DIAG:
+        L.append("s_waitcnt vmcnt(4)")  # the other buffer's 4 loads (issued later) may stay in flight
+    for g in range(2):
+        planes = {b: G(g, b // 4, 1 << (b % 4)) for b in range(8)}
+        transpose({d: RAW(g, d, buf) for d in range(8)}, planes, L)
+    L += [
+        f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1",
+        f"s_cmp_gt_u32 s{S_CNT}, 1",  # row j+2 exists
+        f"s_cselect_b32 s{S_T0}, s{S_INROW}, 0",
+        f"s_add_u32 s{S_SRC}, s{S_SRC}, s{S_T0}",
+        f"s_addc_u32 s{S_SRC + 1}, s{S_SRC + 1}, 0",
+    ]
+    loads(L, buf)
+    for g in range(2):
+        for h in range(2):
+            combos(g, h, L)
+    cur, nxt = S_OFF[buf], S_OFF[1 - buf]
+    L += [
+        "s_waitcnt lgkmcnt(0)",
+        f"s_load_dwordx8 s[{nxt}:{nxt + 7}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
+        f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
+        f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
+        "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)",
+    ]
+    for i in range(NT):
+        L += [
+            f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}",
+            f"s_add_u32 s{S_TGT}, s{S_BASE}, s{cur + i}",
+            f"s_addc_u32 s{S_TGT + 1}, s{S_BASE + 1}, 0",
+            f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]",
+        ]
+    L.append("s_set_gpr_idx_off")
+
+
+def epilogue(L):
+    """Accumulator planes -> bytes (the same involution), into X, stored from there (memory dword d in X + d)."""
+    for i in range(NT):
+        L += [f"s_cmp_gt_u32 s{S_ROWS}, {i}", "s_cbranch_scc0 2f"]
+        for g in range(2):
+            transpose({p: ACC(i, g, p) for p in range(8)}, {d: V_X + d for d in range(8)}, L)
+            for half in range(2):
+                q = 2 * g + half
+                off = f" offset:{q * 1024}" if q else ""
+                L.append(f"global_store_dwordx4 %[off], v[{V_X + 4 * half}:{V_X + 4 * half + 3}], "
+                         f"s[{S_DST}:{S_DST + 1}]{off}")
+        L += [f"s_add_u32 s{S_DST}, s{S_DST}, s{S_OUTROW}", f"s_addc_u32 s{S_DST + 1}, s{S_DST + 1}, 0"]
+    L.append("2:")
+
+
+def program():
+    L = [
+        f"s_mov_b64 s[{S_SRC}:{S_SRC + 1}], %[src]",
+        f"s_mov_b64 s[{S_IDX}:{S_IDX + 1}], %[idx]",
+        f"s_mov_b64 s[{S_DST}:{S_DST + 1}], %[dst]",
+        f"s_mov_b32 s{S_INROW}, %[in_row]",
+        f"s_mov_b32 s{S_OUTROW}, %[out_row]",
+        f"s_mov_b32 s{S_CNT}, %[n_in]",
+        f"s_mov_b32 s{S_ROWS}, %[rows]",
+        f"v_mov_b32 v{V_MASK[0]}, 0xaaaaaaaa",
+        f"v_mov_b32 v{V_MASK[1]}, 0xcccccccc",
+        f"v_mov_b32 v{V_MASK[2]}, 0xf0f0f0f0",
+        f"s_getpc_b64 s[{S_BASE}:{S_BASE + 1}]",
+        "5:",
+        f"s_add_u32 s{S_BASE}, s{S_BASE}, (9f - 5b)",
+        f"s_addc_u32 s{S_BASE + 1}, s{S_BASE + 1}, 0",
+    ]
+    # prologue: source rows 0 and 1 in flight (row 0 again when n_in == 1), block offsets of row 0
+    loads(L, 0)
+    L += [
+        f"s_cmp_gt_u32 s{S_CNT}, 1",
+        f"s_cselect_b32 s{S_T0}, s{S_INROW}, 0",
+        f"s_add_u32 s{S_SRC}, s{S_SRC}, s{S_T0}",
+        f"s_addc_u32 s{S_SRC + 1}, s{S_SRC + 1}, 0",
+    ]
+    loads(L, 1)
+    L.append(f"s_load_dwordx8 s[{S_OFF[0]}:{S_OFF[0] + 7}], s[{S_IDX}:{S_IDX + 1}], 0")
+    L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
+    L += [f"v_mov_b32 {v(G(g, h, 0))}, 0" for g in range(2) for h in range(2)]
+    L.append("1:")
+    body(L, 0)
+    L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f"]
+    body(L, 1)
+    L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc0 1b", "3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    epilogue(L)
+    L.append("s_branch 8f")
+    L.append("9:")
+    blocks(L)
+    L.append("8:")
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "bitslice_jump.inc"))
+    ap.add_argument("--diag", default="", help="comma list: novm (timing diagnostics, wrong results)")
+    args = ap.parse_args()
+    DIAG.update(x for x in args.diag.split(",") if x)
+    lines = program()
+    clob_v = ", ".join(f'"v{r}"' for r in range(LAST_VGPR + 1))
+    clob_s = ", ".join(f'"s{r}"' for r in range(FIRST_SGPR, LAST_SGPR + 1))
+    body_txt = "\\n\\t".join(lines)
+    with open(args.out, "w") as f:
+        f.write("// GENERATED by gen_bsjump.py -- do not edit.  Inner program of gf_matmul_bsj_kernel (kernels.hip).\n")
+        f.write(f"#define RLNC_BSJ_NT {NT}\n")
+        f.write(f"#define RLNC_BSJ_BLOCK_BYTES {BLOCK_BYTES}\n")
+        f.write(f'#define RLNC_BSJ_ASM "{body_txt}"\n')
+        f.write(f"#define RLNC_BSJ_CLOBBER_V {clob_v}\n")
+        f.write(f'#define RLNC_BSJ_CLOBBER_S {clob_s}, "m0", "scc", "memory"\n')
+
+
+if __name__ == "__main__":
+    main()

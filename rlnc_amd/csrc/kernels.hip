@@ -680,6 +680,86 @@ hipError_t launch_bs(const MatmulParams &p, hipStream_t s, void *scratch, size_t
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Bit-sliced variant with one code block per coefficient (gen_bsjump.py has the derivation): the (row,
+// source) work is a call into block c -- 16 v_bitop3_b32 XOR3s with the combination registers baked in and
+// only the accumulator relative to the row slot -- instead of 32 GPR-index-relative XORs + 16 M0 writes.
+// ---------------------------------------------------------------------------------------------------
+#include "bitslice_jump.inc"
+
+constexpr int kBsjRows = RLNC_BSJ_NT;
+static_assert(kBsjRows == kBsRows, "same tiling as gf_matmul_bs_kernel");
+
+// stream[obj][row tile][j][row in tile] = c · RLNC_BSJ_BLOCK_BYTES (c = 0 for rows past n_out)
+__global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, int64_t coef_obj, int64_t coef_row,
+                                                         int n_out, int n_in, int row_tiles, uint32_t *stream) {
+    const int64_t per_obj = int64_t(row_tiles) * n_in * kBsjRows;
+    const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int obj = blockIdx.y;
+    if (e >= per_obj) return;
+    const int i = int(e % kBsjRows);
+    const int j = int((e / kBsjRows) % n_in);
+    const int rt = int(e / (int64_t(kBsjRows) * n_in));
+    const int row = rt * kBsjRows + i;
+    const uint32_t c = row < n_out ? coef[int64_t(obj) * coef_obj + int64_t(row) * coef_row + j] : 0u;
+    stream[int64_t(obj) * row_tiles * n_in * kBsjRows + e] = c * uint32_t(RLNC_BSJ_BLOCK_BYTES);
+}
+
+__global__ __launch_bounds__(kThreads) void gf_matmul_bsj_kernel(MatmulParams p, const uint32_t *stream,
+                                                                 int row_tiles, int col_blocks) {
+    int rt, cb, obj;
+    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    const int row0 = rt * kBsjRows;
+    const int rows = min(kBsjRows, p.n_out - row0);
+    if (p.hdr != nullptr && cb == 0) {
+        Tile t;
+        t.obj = obj;
+        t.cb = 0;
+        t.row0 = row0;
+        t.rows_here = rows;
+        copy_header(p, t);
+    }
+    const uint8_t *src = p.in + int64_t(obj) * p.in_obj + int64_t(cb) * kBsColBlock;
+    uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + int64_t(cb) * kBsColBlock;
+    const uint32_t *idx = stream + (int64_t(obj) * row_tiles + rt) * p.n_in * kBsjRows;
+    const uint32_t off = (threadIdx.x >> 6) * 4096u + (threadIdx.x & 63u) * 16u;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    asm volatile(RLNC_BSJ_ASM
+                 :
+                 : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),
+                   [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows), [off] "v"(off)
+                 : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S);
+#pragma clang diagnostic pop
+}
+
+size_t bsj_scratch_bytes(const MatmulParams &p) {
+    const int64_t tiles = (p.n_out + kBsjRows - 1) / kBsjRows;
+    // + one source: the main loop loads the offsets of the source after the last one
+    return size_t(int64_t(p.n_obj) * tiles * p.n_in * kBsjRows * 4 + 256);
+}
+
+hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full) {
+    full = (p.width / kBsColBlock) * kBsColBlock;
+    const int row_tiles = (p.n_out + kBsjRows - 1) / kBsjRows;
+    const int col_blocks = int(full / kBsColBlock);
+    const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
+    if (scratch == nullptr || scratch_bytes < bsj_scratch_bytes(p)) return hipErrorInvalidValue;
+    if (total > 0x7FFFFFFFLL || p.n_obj > 65535) return hipErrorInvalidValue;
+    uint32_t *stream = static_cast<uint32_t *>(scratch);
+    const int64_t per_obj = int64_t(row_tiles) * p.n_in * kBsjRows;
+    if ((per_obj + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bsj_offset_kernel, dim3(unsigned((per_obj + 255) / 256), unsigned(p.n_obj)), dim3(256), 0, s,
+                       p.coef, p.coef_obj, p.coef_row, p.n_out, p.n_in, row_tiles, stream);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    MatmulParams q = p;
+    q.width = full;
+    hipLaunchKernelGGL(gf_matmul_bsj_kernel, dim3(unsigned(total)), dim3(kThreads), 0, s, q, stream, row_tiles,
+                       col_blocks);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------------
 // element-wise primitives (simd/mod.rs:18-119); the scalar early-outs are taken on the host
 // ---------------------------------------------------------------------------------------------------
 template <int OP, bool ALIGNED>  // OP 0: v = c·v   1: d ^= s   2: d ^= c·s
@@ -809,19 +889,24 @@ static bool matmul_aligned(const MatmulParams &p) {
 }
 
 size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v) {
-    if (v != MatmulVariant::BitSliced || p.n_out <= 0 || p.n_in <= 0 || p.n_obj <= 0) return 0;
-    return bs_eligible(p, matmul_aligned(p)) ? bs_scratch_bytes(p) : 0;
+    if ((v != MatmulVariant::BitSliced && v != MatmulVariant::BitSlicedJump) || p.n_out <= 0 || p.n_in <= 0 ||
+        p.n_obj <= 0)
+        return 0;
+    if (!bs_eligible(p, matmul_aligned(p))) return 0;
+    return v == MatmulVariant::BitSliced ? bs_scratch_bytes(p) : bsj_scratch_bytes(p);
 }
 
 hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, void *scratch, size_t scratch_bytes) {
     if (p.n_out <= 0 || p.width <= 0 || p.n_obj <= 0) return hipSuccess;
     const bool aligned = matmul_aligned(p);
     if (p.n_in <= 0) return hipErrorInvalidValue;
-    if (v == MatmulVariant::BitSliced) {
-        v = MatmulVariant::Perm;  // whatever the bit-sliced kernel does not cover
+    if (v == MatmulVariant::BitSliced || v == MatmulVariant::BitSlicedJump) {
+        const bool jump = v == MatmulVariant::BitSlicedJump;
+        v = MatmulVariant::Perm;  // whatever the bit-sliced kernels do not cover
         if (bs_eligible(p, aligned)) {
             int64_t full = 0;
-            hipError_t e = launch_bs(p, s, scratch, scratch_bytes, full);
+            hipError_t e = jump ? launch_bsj(p, s, scratch, scratch_bytes, full)
+                                : launch_bs(p, s, scratch, scratch_bytes, full);
             if (e != hipSuccess || full == p.width) return e;
             MatmulParams t = p;
             t.in = p.in + full;

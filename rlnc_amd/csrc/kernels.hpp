@@ -28,7 +28,15 @@ struct MatmulParams {
     int n_obj;
 };
 
-enum class MatmulVariant : int { Perm = 0, NibbleLds = 1, Perm3 = 2, Wide = 3, Wide4 = 4, BitSliced = 5 };
+enum class MatmulVariant : int {
+    Perm = 0,
+    NibbleLds = 1,
+    Perm3 = 2,
+    Wide = 3,
+    Wide4 = 4,
+    BitSliced = 5,
+    BitSlicedJump = 6
+};
 
 // Device scratch the BitSliced variant needs for its coefficient-index stream (0 for the others, and for
 // shapes that variant hands to the perm kernel).  launch_matmul fails with hipErrorInvalidValue when a

@@ -12,7 +12,7 @@ from tests.gpu_util import MUL, dev, host, np_matmul
 
 pytestmark = pytest.mark.gpu
 
-DEFAULT_VARIANT = 5  # rlnc_context default (bitsliced, perm for what it does not cover)
+DEFAULT_VARIANT = 6  # rlnc_context default (bit-sliced jump, perm for what it does not cover)
 
 S = ["Ok", "CodingVectorLengthMismatch", "DataLengthMismatch", "PieceCountZero", "DataLengthZero",
      "PieceLengthZero", "NotEnoughPiecesToRecode", "PieceLengthTooShort", "PieceNotUseful", "ReceivedAllPieces",
@@ -68,7 +68,7 @@ SHAPES = [(1, 1, 1, 1), (1, 3, 17, 1), (2, 2, 16, 2), (3, 5, 4095, 1), (4, 32, 4
           (9, 40, 32768, 1)]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("n_out,n_in,W,nobj", SHAPES)
 def test_matmul(ctx, variant, n_out, n_in, W, nobj):
     from rlnc_amd import batch
@@ -97,8 +97,9 @@ BS_SHAPES = [(4, 1, 16384, 1), (5, 2, 16384 + 16, 2), (8, 32, 32768, 1), (9, 31,
              (3, 5, 16384, 1)]
 
 
+@pytest.mark.parametrize("variant", [5, 6])
 @pytest.mark.parametrize("n_out,n_in,W,nobj", BS_SHAPES)
-def test_matmul_bitsliced(ctx, n_out, n_in, W, nobj):
+def test_matmul_bitsliced(ctx, variant, n_out, n_in, W, nobj):
     from rlnc_amd import batch
 
     rng = np.random.default_rng(n_out * 7 + n_in * 3 + W + nobj)
@@ -108,7 +109,7 @@ def test_matmul_bitsliced(ctx, n_out, n_in, W, nobj):
     inp = rng.integers(0, 256, (nobj, n_in, W), dtype=np.uint8)
     inp[:, 0, :256] = np.arange(256, dtype=np.uint8)  # every byte value against every coefficient row
     out = dev(np.zeros((nobj, n_out, W), np.uint8))
-    ctx.set_kernel_variant(5, 0)
+    ctx.set_kernel_variant(variant, 0)
     try:
         batch.matmul(dev(coef), dev(inp), out, ctx)
         got = host(out)
@@ -118,7 +119,28 @@ def test_matmul_bitsliced(ctx, n_out, n_in, W, nobj):
         assert np.array_equal(got[o], np_matmul(coef[o], inp[o])), o
 
 
-def test_matmul_bitsliced_strided_with_header(ctx):
+@pytest.mark.parametrize("variant", [5, 6])
+def test_matmul_every_coefficient(ctx, variant):
+    """All 256 coefficients (16 rows x 16 sources = 0..255) against every byte value: each of the jump
+    variant's 256 code blocks, and every index pattern of the relative-XOR variant."""
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(256)
+    coef = np.arange(256, dtype=np.uint8).reshape(1, 16, 16)
+    inp = rng.integers(0, 256, (1, 16, 16384), dtype=np.uint8)
+    inp[0, :, :256] = np.arange(256, dtype=np.uint8)
+    out = dev(np.zeros((1, 16, 16384), np.uint8))
+    ctx.set_kernel_variant(variant, 0)
+    try:
+        batch.matmul(dev(coef), dev(inp), out, ctx)
+        got = host(out)
+    finally:
+        ctx.set_kernel_variant(DEFAULT_VARIANT, 0)
+    assert np.array_equal(got[0], np_matmul(coef[0], inp[0]))
+
+
+@pytest.mark.parametrize("variant", [5, 6])
+def test_matmul_bitsliced_strided_with_header(ctx, variant):
     """Padded row strides and the coded-piece header copy, through the raw C ABI descriptor."""
     import ctypes as C
 
@@ -138,7 +160,7 @@ def test_matmul_bitsliced_strided_with_header(ctx):
     row = 64 + W + pad
     d = _lib.MatmulDesc(dinp.data_ptr(), n_in * (W + pad), W + pad, dcoef.data_ptr(), n_out * n_in, n_in,
                         base + 64, n_out * row, row, base, n_out * row, row, n_out, n_in, W, nobj)
-    ctx.set_kernel_variant(5, 0)
+    ctx.set_kernel_variant(variant, 0)
     try:
         check(ctx.lib.rlnc_gf256_matmul(ctx.h, C.byref(d)), ctx.lib)
         torch.cuda.synchronize()
