@@ -10,7 +10,12 @@ products of that c as v_bitop3_b32 XOR3s whose combination operands are absolute
 block, only the accumulator (DST and SRC2) relative to the row slot (M0 = 0xC000 | 16 * row).  One call
 costs ~105 cycles at 2 waves/SIMD (scripts/ubench_jump.hip) against ~165 for the relative-XOR form.
 
-Algorithm (one workgroup = 8 output rows x 16 KiB of columns; one lane = 64 bytes as two 32-byte groups):
+Algorithm (one workgroup = 4 waves = 32 output rows x 4 KiB of columns; wave w owns rows 8w..8w+7 of the
+tile; one lane = 64 bytes as two 32-byte groups):
+  * the 4 KiB source chunk of row j reaches LDS once per workgroup, each wave moving a quarter by LDS-DMA
+    (global_load_lds_dwordx4) into a 3-slot ring two rows ahead, one s_barrier per row; every wave then reads
+    the whole chunk with 4 ds_read_b128 (per-CU load traffic is a quarter of 8-row-per-wave tiling's, whose
+    vector-memory path measured ~24 % of the kernel: profiles/r01_bsj_diag.txt);
   * bit-slicing: a group's 8 dwords (32 bytes) are transposed into 8 bit-planes (plane b = bit b of each
     of the 32 bytes) by three delta-swap stages; 64-bit shifts move two registers per instruction and the
     bit-field merges are v_bitop3_b32 (full rate; v_bfi_b32 and 32-bit shifts issue at quarter rate);
@@ -26,9 +31,12 @@ Run `python3 gen_bsjump.py` after editing; the output is committed.
 import argparse
 import os
 
-NT = 8  # output rows per workgroup
-BLOCK_BYTES = 16 * 8 + 4  # 16 VOP3 (8 bytes) + s_setpc_b64 (4 bytes)
-STREAM_J_BYTES = NT * 4  # one dword (block offset) per row
+NT = 8  # output rows per wave
+WAVES = 4  # waves per workgroup (all on the same 4 KiB column chunk)
+WG_ROWS = NT * WAVES
+SLOTS = 3  # LDS ring slots of 4 KiB (rows j, j+1, j+2)
+BLOCK_BYTES = 16 * 8 + 4  # 16 VOP3 (8 bytes) + s_setpc_b64 (4 bytes); --stride pads with s_nop (never run)
+STREAM_J_BYTES = WG_ROWS * 4  # one dword (block offset) per row of the workgroup tile
 
 
 # ---- register map ---------------------------------------------------------------------------------------
@@ -40,21 +48,22 @@ def G(g, h, v):  # combination v of half h of group g (G[g][h][0] = 0)
     return 128 + g * 32 + h * 16 + v
 
 
-def RAW(g, d, buf):  # staging registers: source rows j+1 and j+2 in flight
-    return 192 + 16 * buf + g * 8 + d
+def RAW(g, d):  # the current source row's 64 bytes, read from the LDS ring
+    return 192 + g * 8 + d
 
 
-TMP0 = 224  # 8 temporaries v224..v231 (4 pairs for 64-bit shifts)
-V_X = 232  # 8 registers v232..v239: the transposes' middle stage / the epilogue's store buffer
-V_MASK = (240, 241, 242)  # 0xAAAAAAAA, 0xCCCCCCCC, 0xF0F0F0F0
-LAST_VGPR = 242
-S_OFF = (36, 44)  # two 8-dword block-offset buffers (4-aligned for s_load_dwordx8)
-S_SRC, S_IDX, S_DST, S_BASE, S_TGT, S_RET = 52, 54, 56, 58, 60, 62
-S_INROW, S_OUTROW, S_CNT, S_ROWS, S_T0 = 64, 65, 66, 67, 68
-FIRST_SGPR, LAST_SGPR = S_OFF[0], S_T0
+TMP0 = 208  # 8 temporaries v208..v215 (4 pairs for 64-bit shifts)
+V_X = 216  # 8 registers v216..v223: the transposes' middle stage / the epilogue's store buffer
+V_MASK = (224, 225, 226)  # 0xAAAAAAAA, 0xCCCCCCCC, 0xF0F0F0F0
+LAST_VGPR = 226
+S_OFF = (36, 44, 52)  # block offsets of rows j % 3 (8 dwords each, 4-aligned for s_load_dwordx8)
+S_SRC, S_IDX, S_DST, S_BASE, S_TGT, S_RET = 60, 62, 64, 66, 68, 70
+S_INROW, S_OUTROW, S_CNT, S_ROWS, S_T0, S_LDSW = 72, 73, 74, 75, 76, 77
+FIRST_SGPR, LAST_SGPR = S_OFF[0], S_LDSW
 BFI = "0xca"  # v_bitop3_b32 truth table of S0 ? S1 : S2 (index = S0 S1 S2)
 
 DIAG = set()
+ALIGN = 0  # log2 alignment of the first block (--align)
 
 
 def v(n):
@@ -140,54 +149,88 @@ def blocks(lines):
                 a = ACC(0, g, o)
                 lines.append(f"v_bitop3_b32 v{a}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])}, v{a} bitop3:0x96")
         lines.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+        lines += ["s_nop 0"] * ((BLOCK_BYTES - (16 * 8 + 4)) // 4)
 
 
 # ---- main program ---------------------------------------------------------------------------------------
-def loads(lines, buf):
-    """Source row j+2 into staging buffer `buf` (memory dword d of group g -> RAW(g, d, buf))."""
+def dma(lines, slot):
+    """This wave's quarter (1 KiB) of the row at S_SRC into ring slot `slot` (LDS-DMA: M0 = wave-uniform LDS
+    base, lane l writes base + 16 l; one wait state after the M0 write)."""
     if "novm" in DIAG:
         return
-    for g in range(2):
-        for half in range(2):
-            q = 2 * g + half
-            r0 = RAW(g, 4 * half, buf)
-            off = f" offset:{q * 1024}" if q else ""
-            lines.append(f"global_load_dwordx4 v[{r0}:{r0 + 3}], %[off], s[{S_SRC}:{S_SRC + 1}]{off}")
+    lines += [
+        f"s_add_u32 m0, s{S_LDSW}, {slot * 4096}",
+        "s_nop 0",
+        f"global_load_lds_dwordx4 %[dmaoff], s[{S_SRC}:{S_SRC + 1}]",
+    ]
 
 
-def body(L, buf):
-    if "novm" not in DIAG:
-        L.append("s_waitcnt vmcnt(4)")  # the other buffer's 4 loads (issued later) may stay in flight
-    for g in range(2):
-        planes = {b: G(g, b // 4, 1 << (b % 4)) for b in range(8)}
-        transpose({d: RAW(g, d, buf) for d in range(8)}, planes, L)
-    L += [
-        f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1",
-        f"s_cmp_gt_u32 s{S_CNT}, 1",  # row j+2 exists
+def advance(lines):
+    """S_SRC -> the next source row if it exists (else stays: the re-read is harmless, always in bounds)."""
+    lines += [
+        f"s_cmp_gt_u32 s{S_CNT}, 1",
         f"s_cselect_b32 s{S_T0}, s{S_INROW}, 0",
         f"s_add_u32 s{S_SRC}, s{S_SRC}, s{S_T0}",
         f"s_addc_u32 s{S_SRC + 1}, s{S_SRC + 1}, 0",
     ]
-    loads(L, buf)
+
+
+def body(L, slot):
+    """Source row j (slot = j % 3): its chunk is in ring slot `slot`, its block offsets in S_OFF[slot]."""
+    if "novm" not in DIAG and "novmw" not in DIAG:
+        L.append("s_waitcnt vmcnt(1)")  # this wave's DMA of row j done (row j+1's may stay in flight)
+    if "nobar" not in DIAG:
+        L.append("s_barrier")  # every wave's quarter of row j landed; every wave is done reading row j-1's slot
+    L.append(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
+    advance(L)
+    dma(L, (slot + 2) % SLOTS)  # row j+2 into the slot row j-1 used
     for g in range(2):
         for h in range(2):
-            combos(g, h, L)
-    cur, nxt = S_OFF[buf], S_OFF[1 - buf]
+            q = 2 * g + h
+            if "nods" not in DIAG:
+                L.append(f"ds_read_b128 v[{RAW(g, 4 * h)}:{RAW(g, 4 * h) + 3}], %[ldsr] offset:{slot * 4096 + q * 1024}")
+    if "nosmem" not in DIAG or "nods" not in DIAG:
+        L.append("s_waitcnt lgkmcnt(0)")  # the chunk, and row j's block offsets (SMEM, issued a row earlier)
+    for g in range(2):
+        planes = {b: G(g, b // 4, 1 << (b % 4)) for b in range(8)}
+        if "notrans" in DIAG:  # timing only
+            L += [f"v_mov_b32 v{planes[b]}, v{RAW(g, b)}" for b in range(8)]
+        else:
+            transpose({d: RAW(g, d) for d in range(8)}, planes, L)
+    for g in range(2):
+        for h in range(2):
+            if "nocombo" not in DIAG:
+                combos(g, h, L)
+    cur, nxt = S_OFF[slot], S_OFF[(slot + 1) % SLOTS]
     L += [
-        "s_waitcnt lgkmcnt(0)",
-        f"s_load_dwordx8 s[{nxt}:{nxt + 7}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
+        f"s_load_dwordx8 s[{nxt}:{nxt + 7}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}" if "nosmem" not in DIAG
+        else "s_nop 0",  # timing only: every row reuses the prologue's offsets of rows 0-2
         f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
         f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
-        "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)",
+        "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)" if "absinline" not in DIAG else "s_nop 0",
     ]
     for i in range(NT):
+        if "inline" in DIAG:  # timing only: the products of a fixed coefficient inline, no call
+            L.append(f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}")
+            lo, hi = block_indices(0x53 + i)
+            L += [f"v_bitop3_b32 v{ACC(0, g, o)}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])}, v{ACC(0, g, o)} bitop3:0x96"
+                  for g in range(2) for o in range(8)]
+            continue
+        if "absinline" in DIAG:  # timing only: as "inline" with absolute accumulators (no GPR-index mode)
+            lo, hi = block_indices(0x53 + i)
+            if "nobank" in DIAG:  # ... with the three sources of every XOR3 in three different banks
+                lo = [4 * ((x // 4) % 4) + (o + 1) % 4 for o, x in enumerate(lo)]
+                hi = [4 * ((x // 4) % 4) + (o + 2) % 4 for o, x in enumerate(hi)]
+            L += [f"v_bitop3_b32 v{ACC(i, g, o)}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])}, v{ACC(i, g, o)} bitop3:0x96"
+                  for g in range(2) for o in range(8)]
+            continue
         L += [
             f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}",
             f"s_add_u32 s{S_TGT}, s{S_BASE}, s{cur + i}",
             f"s_addc_u32 s{S_TGT + 1}, s{S_BASE + 1}, 0",
             f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]",
         ]
-    L.append("s_set_gpr_idx_off")
+    L.append("s_set_gpr_idx_off" if "absinline" not in DIAG else "s_nop 0")
 
 
 def epilogue(L):
@@ -221,26 +264,31 @@ def program():
         "5:",
         f"s_add_u32 s{S_BASE}, s{S_BASE}, (9f - 5b)",
         f"s_addc_u32 s{S_BASE + 1}, s{S_BASE + 1}, 0",
+        f"s_mov_b32 s{S_LDSW}, %[ldsw]",
     ]
-    # prologue: source rows 0 and 1 in flight (row 0 again when n_in == 1), block offsets of row 0
-    loads(L, 0)
-    L += [
-        f"s_cmp_gt_u32 s{S_CNT}, 1",
-        f"s_cselect_b32 s{S_T0}, s{S_INROW}, 0",
-        f"s_add_u32 s{S_SRC}, s{S_SRC}, s{S_T0}",
-        f"s_addc_u32 s{S_SRC + 1}, s{S_SRC + 1}, 0",
-    ]
-    loads(L, 1)
+    # prologue: rows 0 and 1 on their way into slots 0 and 1 (row 0 again when n_in == 1), row 0's offsets
+    dma(L, 0)
+    advance(L)
+    dma(L, 1)
     L.append(f"s_load_dwordx8 s[{S_OFF[0]}:{S_OFF[0] + 7}], s[{S_IDX}:{S_IDX + 1}], 0")
+    if "nosmem" in DIAG:
+        L += [f"s_load_dwordx8 s[{S_OFF[b]}:{S_OFF[b] + 7}], s[{S_IDX}:{S_IDX + 1}], {b * STREAM_J_BYTES}"
+              for b in (1, 2)]
+        L.append("s_waitcnt lgkmcnt(0)")
     L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
     L += [f"v_mov_b32 {v(G(g, h, 0))}, 0" for g in range(2) for h in range(2)]
+    # loop over source rows j, three per trip (ring slot and offset buffer j % 3 are immediates)
     L.append("1:")
     body(L, 0)
     L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f"]
     body(L, 1)
+    L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f"]
+    body(L, 2)
     L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc0 1b", "3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
     epilogue(L)
     L.append("s_branch 8f")
+    if ALIGN:
+        L.append(f".p2align {ALIGN}")
     L.append("9:")
     blocks(L)
     L.append("8:")
@@ -248,11 +296,16 @@ def program():
 
 
 def main():
+    global BLOCK_BYTES, ALIGN
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "bitslice_jump.inc"))
-    ap.add_argument("--diag", default="", help="comma list: novm (timing diagnostics, wrong results)")
+    ap.add_argument("--diag", default="", help="comma list: novm, inline, absinline (timing diagnostics, wrong results)")
+    ap.add_argument("--stride", type=int, default=BLOCK_BYTES, help="bytes per code block (>= 132, multiple of 4)")
+    ap.add_argument("--align", type=int, default=0, help="log2 alignment of the block table")
     args = ap.parse_args()
     DIAG.update(x for x in args.diag.split(",") if x)
+    assert args.stride >= BLOCK_BYTES and args.stride % 4 == 0
+    BLOCK_BYTES, ALIGN = args.stride, args.align
     lines = program()
     clob_v = ", ".join(f'"v{r}"' for r in range(LAST_VGPR + 1))
     clob_s = ", ".join(f'"s{r}"' for r in range(FIRST_SGPR, LAST_SGPR + 1))
@@ -260,6 +313,8 @@ def main():
     with open(args.out, "w") as f:
         f.write("// GENERATED by gen_bsjump.py -- do not edit.  Inner program of gf_matmul_bsj_kernel (kernels.hip).\n")
         f.write(f"#define RLNC_BSJ_NT {NT}\n")
+        f.write(f"#define RLNC_BSJ_WAVES {WAVES}\n")
+        f.write(f"#define RLNC_BSJ_SLOTS {SLOTS}\n")
         f.write(f"#define RLNC_BSJ_BLOCK_BYTES {BLOCK_BYTES}\n")
         f.write(f'#define RLNC_BSJ_ASM "{body_txt}"\n')
         f.write(f"#define RLNC_BSJ_CLOBBER_V {clob_v}\n")

@@ -684,10 +684,16 @@ hipError_t launch_bs(const MatmulParams &p, hipStream_t s, void *scratch, size_t
 // source) work is a call into block c -- 16 v_bitop3_b32 XOR3s with the combination registers baked in and
 // only the accumulator relative to the row slot -- instead of 32 GPR-index-relative XORs + 16 M0 writes.
 // ---------------------------------------------------------------------------------------------------
+#ifdef RLNC_BSJ_ASM_FILE  // diagnostic builds substitute a generated variant
+#include RLNC_BSJ_ASM_FILE
+#else
 #include "bitslice_jump.inc"
+#endif
 
-constexpr int kBsjRows = RLNC_BSJ_NT;
-static_assert(kBsjRows == kBsRows, "same tiling as gf_matmul_bs_kernel");
+constexpr int kBsjWaveRows = RLNC_BSJ_NT;                   // output rows per wave
+constexpr int kBsjRows = RLNC_BSJ_NT * RLNC_BSJ_WAVES;        // output rows per workgroup tile
+constexpr int kBsjColBlock = 4096;                            // 64 lanes × 64 B, shared by the 4 waves
+static_assert(RLNC_BSJ_WAVES * 64 == kThreads, "one wave per 8-row slice of the tile");
 
 // stream[obj][row tile][j][row in tile] = c · RLNC_BSJ_BLOCK_BYTES (c = 0 for rows past n_out)
 __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, int64_t coef_obj, int64_t coef_row,
@@ -701,11 +707,12 @@ __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, in
     const int rt = int(e / (int64_t(kBsjRows) * n_in));
     const int row = rt * kBsjRows + i;
     const uint32_t c = row < n_out ? coef[int64_t(obj) * coef_obj + int64_t(row) * coef_row + j] : 0u;
-    stream[int64_t(obj) * row_tiles * n_in * kBsjRows + e] = c * uint32_t(RLNC_BSJ_BLOCK_BYTES);
+    stream[int64_t(obj) * per_obj + e] = c * uint32_t(RLNC_BSJ_BLOCK_BYTES);
 }
 
 __global__ __launch_bounds__(kThreads) void gf_matmul_bsj_kernel(MatmulParams p, const uint32_t *stream,
                                                                  int row_tiles, int col_blocks) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[RLNC_BSJ_SLOTS * kBsjColBlock];
     int rt, cb, obj;
     decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
     const int row0 = rt * kBsjRows;
@@ -718,18 +725,35 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_bsj_kernel(MatmulParams p,
         t.rows_here = rows;
         copy_header(p, t);
     }
-    const uint8_t *src = p.in + int64_t(obj) * p.in_obj + int64_t(cb) * kBsColBlock;
-    uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + int64_t(cb) * kBsColBlock;
-    const uint32_t *idx = stream + (int64_t(obj) * row_tiles + rt) * p.n_in * kBsjRows;
-    const uint32_t off = (threadIdx.x >> 6) * 4096u + (threadIdx.x & 63u) * 16u;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const int rows_w = __builtin_amdgcn_readfirstlane(max(0, min(kBsjWaveRows, rows - kBsjWaveRows * w)));
+    const uint8_t *src = p.in + int64_t(obj) * p.in_obj + int64_t(cb) * kBsjColBlock;
+    uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0 + kBsjWaveRows * w) * p.out_row +
+                   int64_t(cb) * kBsjColBlock;
+    const uint32_t *idx = stream + (int64_t(obj) * row_tiles + rt) * p.n_in * kBsjRows + kBsjWaveRows * w;
+    // LDS byte address of the ring (address-space-3 pointer value)
+    typedef __attribute__((address_space(3))) uint8_t lds_u8;
+    const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)ring));  // addrspacecast
+    const uint32_t ldsw = __builtin_amdgcn_readfirstlane(ring_lds + 1024u * uint32_t(w));
+    const uint32_t ldsr = ring_lds + 16u * lane;
+    const uint32_t dmaoff = 1024u * uint32_t(w) + 16u * lane;
+    const uint32_t off = 16u * lane;
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
     asm volatile(RLNC_BSJ_ASM
                  :
                  : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),
-                   [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows), [off] "v"(off)
+                   [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw),
+                   [off] "v"(off), [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr)
                  : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S);
 #pragma clang diagnostic pop
+}
+
+// Whole 4 KiB column blocks of 16-byte-aligned operands; the ragged tail goes to the perm kernel.
+bool bsj_eligible(const MatmulParams &p, bool aligned) {
+    return aligned && p.width >= kBsjColBlock && p.n_out >= 4 && p.in_row < (int64_t(1) << 32) &&
+           p.out_row < (int64_t(1) << 32);
 }
 
 size_t bsj_scratch_bytes(const MatmulParams &p) {
@@ -739,9 +763,9 @@ size_t bsj_scratch_bytes(const MatmulParams &p) {
 }
 
 hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full) {
-    full = (p.width / kBsColBlock) * kBsColBlock;
+    full = (p.width / kBsjColBlock) * kBsjColBlock;
     const int row_tiles = (p.n_out + kBsjRows - 1) / kBsjRows;
-    const int col_blocks = int(full / kBsColBlock);
+    const int col_blocks = int(full / kBsjColBlock);
     const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
     if (scratch == nullptr || scratch_bytes < bsj_scratch_bytes(p)) return hipErrorInvalidValue;
     if (total > 0x7FFFFFFFLL || p.n_obj > 65535) return hipErrorInvalidValue;
@@ -892,8 +916,8 @@ size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v) {
     if ((v != MatmulVariant::BitSliced && v != MatmulVariant::BitSlicedJump) || p.n_out <= 0 || p.n_in <= 0 ||
         p.n_obj <= 0)
         return 0;
-    if (!bs_eligible(p, matmul_aligned(p))) return 0;
-    return v == MatmulVariant::BitSliced ? bs_scratch_bytes(p) : bsj_scratch_bytes(p);
+    if (v == MatmulVariant::BitSliced) return bs_eligible(p, matmul_aligned(p)) ? bs_scratch_bytes(p) : 0;
+    return bsj_eligible(p, matmul_aligned(p)) ? bsj_scratch_bytes(p) : 0;
 }
 
 hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, void *scratch, size_t scratch_bytes) {
@@ -903,7 +927,7 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
     if (v == MatmulVariant::BitSliced || v == MatmulVariant::BitSlicedJump) {
         const bool jump = v == MatmulVariant::BitSlicedJump;
         v = MatmulVariant::Perm;  // whatever the bit-sliced kernels do not cover
-        if (bs_eligible(p, aligned)) {
+        if (jump ? bsj_eligible(p, aligned) : bs_eligible(p, aligned)) {
             int64_t full = 0;
             hipError_t e = jump ? launch_bsj(p, s, scratch, scratch_bytes, full)
                                 : launch_bs(p, s, scratch, scratch_bytes, full);

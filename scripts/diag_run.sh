@@ -7,6 +7,6 @@ for rep in 1 2; do
   for d in product ${DIAGS:-novm nosmem novm_nosmem}; do
     if [ $d = product ]; then unset RLNC_LIB_PATH; else export RLNC_LIB_PATH=build/diag_$d/librlnc_hip.so; fi
     echo "== $d"
-    RLNC_DIAG=1 timeout -k 10 120 python scripts/sweep.py --configs 5:0 --rounds ${ROUNDS:-10} 2>&1 | grep -v amdgpu.ids || exit $?
+    RLNC_DIAG=1 timeout -k 10 120 python scripts/sweep.py --configs ${CONFIGS:-6:0} --rounds ${ROUNDS:-10} 2>&1 | grep -v amdgpu.ids || exit $?
   done
 done

@@ -11,8 +11,8 @@ for d in product ${DIAGS:-}; do
   rm -rf "$OUT"; mkdir -p "$OUT"
   if [ $d = product ]; then unset RLNC_LIB_PATH; else export RLNC_LIB_PATH=$ROOT/build/diag_$d/librlnc_hip.so; fi
   (cd /tmp && RLNC_DIAG=1 timeout -k 10 -s KILL 120 rocprofv3 --kernel-trace --pmc $CNT -d "$OUT" -o run --output-format csv -- \
-      python3 "$ROOT/scripts/sweep.py" --configs 5:0 --rounds 2 > "$OUT/log" 2>&1)
+      python3 "$ROOT/scripts/sweep.py" --configs ${CONFIGS:-6:0} --rounds 2 > "$OUT/log" 2>&1)
   rc=$?; echo "== $d rc=$rc"
   [ $rc -ne 0 ] && { tail -5 "$OUT/log"; exit $rc; }
-  python3 "$ROOT/scripts/pmc_summary.py" "$OUT" | grep bs_kernel
+  python3 "$ROOT/scripts/pmc_summary.py" "$OUT" | grep -E "bs_kernel|bsj_kernel"
 done

@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--objects", type=int, default=16)
     ap.add_argument("--configs", default="0:0,0:16,0:8,1:0")
+    ap.add_argument("--fill", default="random", choices=["random", "zero", "ones"],
+                    help="source bytes (zero/ones: the data-dependent power/clock check of MI355X_MICROARCH.md)")
     args = ap.parse_args()
     import torch
 
@@ -30,6 +32,8 @@ def main():
     g = torch.Generator(device="cuda")
     g.manual_seed(1)
     src = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device="cuda", generator=g)
+    if args.fill != "random":
+        src.fill_(0 if args.fill == "zero" else 0xFF)
     co = torch.randint(0, 256, (B, n, k), dtype=torch.uint8, device="cuda", generator=g)
     out = torch.empty((B, n, k + L), dtype=torch.uint8, device="cuda")
     T = torch.randint(0, 256, (B, k, k), dtype=torch.uint8, device="cuda", generator=g)
