@@ -110,8 +110,9 @@ int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc);
  * max_tile_rows caps the output rows per launch/workgroup (0 = automatic, else 1/2/4/8/16/32). */
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows);
 /* Where rlnc_decode_batch runs the coefficient elimination: 0 = auto (device when it fits LDS, default),
- * 1 = host threads, 2 = device, 3 = device with the clean-state steps on LDS instead of registers.  All are
- * exact replicas; the switch exists for A/B tests. */
+ * 1 = host threads, 2 = device, 3 = device with the clean-state steps on LDS instead of registers, 4 = device
+ * with the clean-state steps on one wave's registers (2 spreads the initial clean run over 4 waves when k <= 32).
+ * All are exact replicas; the switch exists for A/B tests. */
 int rlnc_set_decode_path(rlnc_context *ctx, int path);
 
 /* ---- Encoder: src/full/encoder.rs ----------------------------------------------------------------- */

@@ -47,7 +47,8 @@ class Context:
         check(self.lib.rlnc_context_synchronize(self.h), self.lib)
 
     def set_decode_path(self, path: int = 0):
-        """0 auto, 1 host elimination, 2 device elimination (both exact)."""
+        """0 auto, 1 host elimination, 2 device elimination, 3 device with the clean state on LDS, 4 device on
+        one wave's registers (all exact; 2-4 exist for A/B)."""
         check(self.lib.rlnc_set_decode_path(self.h, int(path)), self.lib)
 
     def set_kernel_variant(self, variant: int = 6, max_tile_rows: int = 0):

@@ -105,7 +105,8 @@ struct rlnc_context {
     rlnc::MatmulVariant variant = rlnc::MatmulVariant::BitSlicedJump;
     int max_tile_rows = 0;
     int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination,
-                          // 3 device elimination with the clean state on LDS (A/B)
+                          // 3 device elimination with the clean state on LDS, 4 ... on one wave's
+                          // registers (A/B)
     DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len, ws_pstat, ws_rank, ws_idx;
     PinBuf pin_a, pin_b, pin_c;
 
@@ -323,7 +324,7 @@ int rlnc_context_synchronize(rlnc_context *ctx) {
 }
 
 int rlnc_set_decode_path(rlnc_context *ctx, int path) {
-    CHECK_ARG(ctx != nullptr && path >= 0 && path <= 3);
+    CHECK_ARG(ctx != nullptr && path >= 0 && path <= 4);
     ctx->decode_path = path;
     return RLNC_OK;
 }
@@ -827,7 +828,7 @@ static int decode_batch_device_impl(rlnc_context *ctx, const uint8_t *pieces, si
     rp.T_obj = int64_t(k * m);
     rp.status = pstat_dev;
     rp.rank = rank_dev;
-    rp.lds_only = ctx->decode_path == 3 ? 1 : 0;
+    rp.lds_only = ctx->decode_path == 3 ? 1 : ctx->decode_path == 4 ? 2 : 0;
     HIP_TRY(rlnc::launch_rref_batch(rp, ctx->stream));
     rlnc::MatmulParams p{};
     p.in = pieces + k;

@@ -147,7 +147,12 @@ def blocks(lines):
         for g in range(2):
             for o in range(8):
                 a = ACC(0, g, o)
-                lines.append(f"v_bitop3_b32 v{a}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])}, v{a} bitop3:0x96")
+                if lo[o] == 0 and hi[o] == 0:  # nothing to add: keep the block size (8 bytes), issue no VALU
+                    lines += ["s_nop 0", "s_nop 0"]
+                    continue
+                x = f"v{G(g, 0, lo[o])}" if lo[o] else "0"  # G[.][0] = 0: an inline constant reads no VGPR bank
+                y = f"v{G(g, 1, hi[o])}" if hi[o] else "0"
+                lines.append(f"v_bitop3_b32 v{a}, {x}, {y}, v{a} bitop3:0x96")
         lines.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
         lines += ["s_nop 0"] * ((BLOCK_BYTES - (16 * 8 + 4)) // 4)
 

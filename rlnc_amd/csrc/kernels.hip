@@ -836,9 +836,13 @@ hipError_t launch_vec(uint8_t *dst, const uint8_t *src, int64_t len, uint8_t c, 
 // encoder.rs:95-99), so the scan normally stops after one chunk — O(1) instead of a full re-read.
 template <bool ALIGNED>
 __global__ __launch_bounds__(64) void last_nonzero_kernel(const uint8_t *data, int64_t obj_stride, int64_t len,
-                                                          unsigned long long *best) {
+                                                          unsigned long long *best, const int32_t *rank, int k) {
     const int obj = blockIdx.x;
     const int lane = threadIdx.x;
+    if (rank != nullptr && rank[obj] < k) {  // not decoded: NotAllPiecesReceivedYet, no data to scan
+        if (lane == 0) best[obj] = 0;
+        return;
+    }
     const uint8_t *d = data + int64_t(obj) * obj_stride;
     for (int64_t c = (len + 1023) / 1024 - 1; c >= 0; --c) {
         const int64_t off = c * 1024 + int64_t(lane) * kBytesPerThread;
@@ -897,9 +901,11 @@ hipError_t launch_final_data_len_ranked(const uint8_t *data, int64_t obj_stride,
                                         int64_t *final_len, hipStream_t s) {
     if (n_obj <= 0) return hipSuccess;
     if (al16(data) && (n_obj == 1 || al16(obj_stride)))
-        hipLaunchKernelGGL(last_nonzero_kernel<true>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch);
+        hipLaunchKernelGGL(last_nonzero_kernel<true>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch, rank,
+                           k);
     else
-        hipLaunchKernelGGL(last_nonzero_kernel<false>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch);
+        hipLaunchKernelGGL(last_nonzero_kernel<false>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch, rank,
+                           k);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(final_len_ranked_kernel, dim3((n_obj + 255) / 256), dim3(256), 0, s, data, obj_stride, n_obj, k,
@@ -971,9 +977,11 @@ hipError_t launch_final_data_len(const uint8_t *data, int64_t obj_stride, int64_
     if (n_obj <= 0) return hipSuccess;
     hipError_t e;
     if (al16(data) && (n_obj == 1 || al16(obj_stride)))
-        hipLaunchKernelGGL(last_nonzero_kernel<true>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch);
+        hipLaunchKernelGGL(last_nonzero_kernel<true>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch,
+                           nullptr, 0);
     else
-        hipLaunchKernelGGL(last_nonzero_kernel<false>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch);
+        hipLaunchKernelGGL(last_nonzero_kernel<false>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch,
+                           nullptr, 0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(final_len_kernel, dim3((n_obj + 255) / 256), dim3(256), 0, s, data, obj_stride, n_obj, scratch,
                        status, final_len, invalid_code);

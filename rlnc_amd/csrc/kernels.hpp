@@ -68,7 +68,7 @@ struct RrefParams {
     int64_t T_obj;
     int32_t *status;
     int32_t *rank;
-    int lds_only;  // 1: keep the clean state on LDS (A/B of the two exact paths), 0: registers when they fit
+    int lds_only;  // clean-state path (A/B, all exact): 0 registers, multi-wave when it fits; 1 LDS; 2 registers, one wave
 };
 constexpr size_t kRrefMaxLds = 160 * 1024;
 size_t rref_lds_bytes(int k, int m);

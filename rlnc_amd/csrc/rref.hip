@@ -542,12 +542,125 @@ __device__ int reg_run(const Mat &M, const uint32_t *tab, uint32_t (&v)[RT], con
 }
 
 // staged headers: m × k bytes after the matrix (hdr_lds = 1), else read from global memory per piece
-// G > 0: the clean state runs on registers (reg_run<G, RT>); G = 0: on LDS (clean_append)
-template <int G, int RT>
-__global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p, int hdr_lds) {
+// ---------------------------------------------------------------------------------------------------
+// Multi-wave clean run (k <= 32, row <= 16 dwords): the same products as reg_run, with the matrix rows spread
+// over NW waves (wave s, lane (w, g), register t holds dword w of row 8s + 4t + g).  Per piece: each wave's
+// forward partial sum is reduced inside the wave, the NW partials meet in LDS (one barrier per piece, two
+// buffers), every wave finishes the new row redundantly, then updates its own rows (backward).  A wave's VALU
+// work per piece is 1/NW of the single-wave path's.  Returns the next piece index; on exit (all pieces done,
+// or a kept row with a zero diagonal ends the clean state) the whole matrix is in LDS.
+// ---------------------------------------------------------------------------------------------------
+template <int NW>
+__device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, uint32_t *P, int m, int k, int &rows,
+                          bool &clean, int32_t *St) {
+    constexpr int G = 4, DP = 16, RTW = 2;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int w = lane % DP, g = lane / DP;
+    const bool wl = w < M.D;
+    uint32_t cm = 0;  // coefficient bytes (< k) of this lane's dword
+    if (wl && 4 * w < k) cm = 4 * w + 4 <= k ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (8 * (4 * w + 4 - k)));
+    uint32_t v[RTW] = {0u, 0u};
+    auto row_of = [&](int t) { return 8 * wave + G * t + g; };
+    // forward operands of piece pc for row count r: init dword w and the tables of M[r][i] for own rows i
+    uint32_t init = 0, t2[RTW];
+    uint4 t4[RTW];
+    auto load_ops = [&](int pc, int r) {
+        const uint8_t *h = H + pc * k;
+        uint32_t q[RTW];
+#pragma unroll
+        for (int t = 0; t < RTW; ++t) q[t] = row_of(t) < r ? uint32_t(h[row_of(t)]) : 0u;
+        uint32_t x = 0;
+        if (wl) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int c = 4 * w + b;
+                x |= (c < k ? uint32_t(h[c]) : uint32_t(c == k + pc)) << (8 * b);
+            }
+        }
+        init = x;
+#pragma unroll
+        for (int t = 0; t < RTW; ++t) {
+            t4[t] = *reinterpret_cast<const uint4 *>(tab + q[t] * kTabDw);
+            t2[t] = tab[q[t] * kTabDw + 4];
+        }
+    };
+    auto to_lds = [&](int nrows) {
+#pragma unroll
+        for (int t = 0; t < RTW; ++t)
+            if (row_of(t) < nrows && wl) M.w[row_of(t) * M.D + w] = v[t];
+    };
+    int buf = 0, pc = 0;
+    load_ops(0, 0);
+    for (; pc < m; ++pc) {
+        const int r = rows;
+        if (r == k) {  // decoder.rs:97-99
+            if (threadIdx.x == 0) St[pc] = RLNC_ERR_RECEIVED_ALL_PIECES;
+            continue;
+        }
+        uint32_t acc = 0;
+#pragma unroll
+        for (int t = 0; t < RTW; ++t) acc ^= mul4t(t4[t], t2[t], v[t]);
+        acc ^= __shfl_xor(acc, 16);
+        acc ^= __shfl_xor(acc, 32);
+        uint32_t *Pb = P + buf * NW * DP;
+        if (lane < DP) Pb[wave * DP + lane] = acc;
+        __syncthreads();
+        uint32_t nr = init;
+#pragma unroll
+        for (int s = 0; s < NW; ++s) nr ^= Pb[s * DP + w];
+        buf ^= 1;
+        const int rw = r >> 2, rb = 8 * (r & 3);
+        const uint32_t piv = (__builtin_amdgcn_readlane(nr, rw) >> rb) & 0xFFu;
+        if (piv == 0) {
+            const bool keep = ballot((nr & cm) != 0) != 0;  // remove_zero_rows (:222-244)
+            if (threadIdx.x == 0) St[pc] = keep ? RLNC_OK : RLNC_ERR_PIECE_NOT_USEFUL;
+            if (keep) {  // leave the clean state: the matrix goes to LDS for the single-wave generic path
+                to_lds(r);
+                if (wave == 0 && g == 0 && wl) M.w[r * M.D + w] = nr;
+                __syncthreads();
+                rows = r + 1;
+                clean = false;
+                return pc + 1;
+            }
+            if (pc + 1 < m) load_ops(pc + 1, r);
+            continue;
+        }
+        const uint4 ti4 = *reinterpret_cast<const uint4 *>(tab + (256 + piv) * kTabDw);
+        const uint32_t ti2 = tab[(256 + piv) * kTabDw + 4];
+        const uint32_t mask = from_mask(w, r + 1);
+        nr = (nr & ~mask) | (mul4t(ti4, ti2, nr) & mask);
+        if (w == rw) nr = (nr & ~(0xFFu << rb)) | (1u << rb);
+        uint4 b4[RTW];
+        uint32_t b2[RTW];
+#pragma unroll
+        for (int t = 0; t < RTW; ++t) {
+            const uint32_t qb = (__shfl(v[t], rw + DP * g) >> rb) & 0xFFu;  // M[row][r], row in this wave
+            b4[t] = *reinterpret_cast<const uint4 *>(tab + qb * kTabDw);
+            b2[t] = tab[qb * kTabDw + 4];
+        }
+        rows = r + 1;
+        if (pc + 1 < m) load_ops(pc + 1, r + 1);
+#pragma unroll
+        for (int t = 0; t < RTW; ++t) v[t] ^= mul4t(b4[t], b2[t], nr);
+#pragma unroll
+        for (int t = 0; t < RTW; ++t)
+            if (row_of(t) == r) v[t] = nr;
+        if (threadIdx.x == 0) St[pc] = RLNC_OK;
+    }
+    to_lds(rows);
+    __syncthreads();
+    return pc;
+}
+
+// G > 0: the clean state runs on registers (reg_run<G, RT>); G = 0: on LDS (clean_append).  NW > 1: the
+// initial clean run is spread over NW waves (reg_run_mw); then waves 1..NW-1 end and wave 0 continues alone
+// (S_BARRIER waits only for the waves that have not terminated).
+template <int G, int RT, int NW>
+__global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, int hdr_lds) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;  // kTabEntries × kTabDw dwords
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x;  // the single-wave code below runs in wave 0 only (lane < 64)
+    const int tid = threadIdx.x;
     const int o = blockIdx.x;
     const int k = p.k, m = p.m;
 #ifdef RLNC_RREF_PROFILE  // diagnostic build: statuses become per-piece cycle counts, rank the setup cycles
@@ -562,45 +675,59 @@ __global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p, int hdr
     // its release fence wait for the store to reach memory, once per piece
     int32_t *St = reinterpret_cast<int32_t *>(M.b + size_t(k + 1) * M.S);
     uint8_t *H = reinterpret_cast<uint8_t *>(St + ((m + 3) & ~3));
+    // NW > 1: two buffers of NW × 16 forward partial sums after the staged headers
+    uint32_t *P = reinterpret_cast<uint32_t *>(H + ((size_t(m) * k + 15) & ~size_t(15)));
 
     {  // all loads of the table copy in flight at once (one memory latency, not one per iteration)
-        constexpr int kPer = kTabEntries * kTabDw / 4 / 64;
+        constexpr int kPer = kTabEntries * kTabDw / 4 / (64 * NW);
         const uint4 *src = reinterpret_cast<const uint4 *>(kRrefTable.v);
         uint4 *dst = reinterpret_cast<uint4 *>(tab);
         uint4 t4[kPer];
 #pragma unroll
-        for (int u = 0; u < kPer; ++u) t4[u] = src[lane + 64 * u];
+        for (int u = 0; u < kPer; ++u) t4[u] = src[tid + 64 * NW * u];
 #pragma unroll
-        for (int u = 0; u < kPer; ++u) dst[lane + 64 * u] = t4[u];
+        for (int u = 0; u < kPer; ++u) dst[tid + 64 * NW * u] = t4[u];
     }
     const uint8_t *base = p.pieces + int64_t(o) * p.obj_stride;
     if (hdr_lds) {  // 16 independent byte loads in flight per batch
-        for (int e0 = 0; e0 < m * k; e0 += 64 * 16) {
+        for (int e0 = 0; e0 < m * k; e0 += 64 * NW * 16) {
             uint8_t hb[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
-                const int e = e0 + lane + 64 * u;
+                const int e = e0 + tid + 64 * NW * u;
                 hb[u] = e < m * k ? base[int64_t(e / k) * p.piece_stride + e % k] : uint8_t(0);
             }
 #pragma unroll
             for (int u = 0; u < 16; ++u)
-                if (e0 + lane + 64 * u < m * k) H[e0 + lane + 64 * u] = hb[u];
+                if (e0 + tid + 64 * NW * u < m * k) H[e0 + tid + 64 * NW * u] = hb[u];
         }
     }
-    for (int w = lane; w < (k + 1) * M.D; w += 64) M.w[w] = 0;
+    for (int w = tid; w < (k + 1) * M.D; w += 64 * NW) M.w[w] = 0;
     __syncthreads();
 
     int rows = 0;
     bool clean = true;
-    uint32_t v[G > 0 ? RT : 1];
-#pragma unroll
-    for (int t = 0; t < (G > 0 ? RT : 1); ++t) v[t] = 0;
+    int pc0 = 0;
 #ifdef RLNC_RREF_PROFILE
     const uint64_t t_setup = __builtin_amdgcn_s_memtime();
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t prof_t = t_setup;
 #endif
-    for (int pc = 0; pc < m; ++pc) {
+    if constexpr (NW > 1) {
+        pc0 = reg_run_mw<NW>(M, tab, H, P, m, k, rows, clean, St);
+        if (threadIdx.x >= 64) return;  // wave 0 finishes alone (generic path / output)
+#ifdef RLNC_RREF_PROFILE  // diagnostic: slot 0 = setup cycles, slot 1 = the multi-wave clean run
+        prof[0] = t_setup - t_start;
+        prof[1] = __builtin_amdgcn_s_memtime() - t_setup;
+        prof_t = __builtin_amdgcn_s_memtime();
+#endif
+    }
+    uint32_t v[G > 0 ? RT : 1];
+#pragma unroll
+    for (int t = 0; t < (G > 0 ? RT : 1); ++t) v[t] = 0;
+    if constexpr (NW > 1)
+        if (clean && rows > 0 && pc0 < m) lds_to_regs<G, RT>(M, v, rows);
+    for (int pc = pc0; pc < m; ++pc) {
         if constexpr (G > 0) {
             if (clean) {
                 pc = reg_run<G, RT>(M, tab, v, H, pc, m, k, rows, clean, St PROF_PASS);
@@ -640,7 +767,7 @@ __global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p, int hdr
         PROF_MARK(7);
     }
     if constexpr (G > 0)
-        if (clean) regs_to_lds<G, RT>(M, v, rows);
+        if (clean && pc0 < m) regs_to_lds<G, RT>(M, v, rows);
     __syncthreads();
 #ifdef RLNC_RREF_PROFILE  // phases: 0 row init, 1 spare copy, 2 forward, 3 normalise, 4 backward, 5 generic, 6 is_clean, 7 status
     if (lane == 0)
@@ -665,7 +792,10 @@ __global__ __launch_bounds__(64) void gf_rref_batch_kernel(RrefParams p, int hdr
 size_t rref_lds_bytes(int k, int m) {
     return kTabEntries * kTabDw * 4 + size_t(k + 1) * 4 * size_t(rref_row_dwords(k, m)) + 4 * ((size_t(m) + 3) & ~size_t(3));
 }
-static size_t rref_lds_bytes_staged(int k, int m) { return rref_lds_bytes(k, m) + ((size_t(k) * m + 15) & ~size_t(15)); }
+// + the staged headers, + 2 × 4 × 16 dwords of multi-wave partial sums
+static size_t rref_lds_bytes_staged(int k, int m) {
+    return rref_lds_bytes(k, m) + ((size_t(k) * m + 15) & ~size_t(15)) + 2 * 4 * 16 * 4;
+}
 
 hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     if (p.n_obj <= 0) return hipSuccess;
@@ -673,25 +803,30 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     if (lds > kRrefMaxLds) return hipErrorInvalidValue;
     const int hdr_lds = rref_lds_bytes_staged(p.k, p.m) <= kRrefMaxLds ? 1 : 0;
     if (hdr_lds) lds = rref_lds_bytes_staged(p.k, p.m);
-    // register-resident clean path when the matrix fits: rows <= G·RT, row dwords <= 64 / G
+    // register-resident clean path when the matrix fits: rows <= G·RT, row dwords <= 64 / G; the initial clean
+    // run spread over 4 waves when k <= 32 and rows are <= 16 dwords
     const int D = rref_row_dwords(p.k, p.m);
-    auto kern = &gf_rref_batch_kernel<0, 1>;
-    if (!p.lds_only && hdr_lds) {  // the register path reads the staged headers
-        if (D <= 16 && p.k <= 32)
-            kern = &gf_rref_batch_kernel<4, 8>;
-        else if (D <= 32 && p.k <= 64)
-            kern = &gf_rref_batch_kernel<2, 32>;
+    auto kern = &gf_rref_batch_kernel<0, 1, 1>;
+    int threads = 64;
+    if (p.lds_only != 1 && hdr_lds) {  // the register paths read the staged headers
+        if (D <= 16 && p.k <= 32) {
+            kern = p.lds_only == 0 ? &gf_rref_batch_kernel<4, 8, 4> : &gf_rref_batch_kernel<4, 8, 1>;
+            threads = p.lds_only == 0 ? 256 : 64;
+        } else if (D <= 32 && p.k <= 64) {
+            kern = &gf_rref_batch_kernel<2, 32, 1>;
+        }
     }
     static bool attr_set = false;
     if (!attr_set) {
-        for (auto f : {&gf_rref_batch_kernel<0, 1>, &gf_rref_batch_kernel<4, 8>, &gf_rref_batch_kernel<2, 32>}) {
+        for (auto f : {&gf_rref_batch_kernel<0, 1, 1>, &gf_rref_batch_kernel<4, 8, 1>, &gf_rref_batch_kernel<4, 8, 4>,
+                       &gf_rref_batch_kernel<2, 32, 1>}) {
             hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(f),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, int(kRrefMaxLds));
             if (e != hipSuccess) return e;
         }
         attr_set = true;
     }
-    hipLaunchKernelGGL(kern, dim3(p.n_obj), dim3(64), lds, s, p, hdr_lds);
+    hipLaunchKernelGGL(kern, dim3(p.n_obj), dim3(threads), lds, s, p, hdr_lds);
     return hipGetLastError();
 }
 

@@ -42,7 +42,8 @@ def main():
     dirty[:, 1, :] = 0
     dirty[:, 1, 2] = 5  # reduced by row 0 (column 0 is zero) -> diagonal M[1][1] = 0, column 2 nonzero: kept
     cases["dirty_from_piece_1"] = dirty
-    paths = [int(x) for x in os.environ.get("RREF_PATHS", "2,3").split(",")]  # 2 registers, 3 LDS clean state
+    # 2 registers (multi-wave initial clean run), 3 LDS clean state, 4 registers on one wave
+    paths = [int(x) for x in os.environ.get("RREF_PATHS", "2,4,3").split(",")]
     for (name, co), path in [(c, p) for c in cases.items() for p in paths]:
         ctx.set_decode_path(path)
         pieces = torch.empty((B, m, k + L), dtype=torch.uint8, device="cuda")

@@ -262,7 +262,7 @@ def test_golden_decode_object_api(ctx, golden):
             assert e.name == v["final_status"], v["name"]
 
 
-@pytest.mark.parametrize("path", [1, 2, 3])
+@pytest.mark.parametrize("path", [1, 2, 3, 4])
 def test_golden_decode_batch(ctx, golden, path):
     from rlnc_amd import batch
 
@@ -302,7 +302,7 @@ def _sequences(rng, nobj, k, m, L, sparsity, dep_frac):
     return seqs
 
 
-@pytest.mark.parametrize("path", [1, 2, 3])
+@pytest.mark.parametrize("path", [1, 2, 3, 4])
 @pytest.mark.parametrize("k,m,L,sparsity,dep", [(32, 32, 40, 0.0, 0.0), (64, 64, 24, 0.0, 0.1),
                                                 (48, 56, 10, 0.4, 0.1), (64, 70, 9, 0.85, 0.05), (8, 14, 5, 0.7, 0.1), (8, 12, 33, 0.9, 0.0), (32, 40, 64, 0.0, 0.2),
                                                 (32, 36, 16, 0.6, 0.1), (17, 30, 7, 0.5, 0.2), (70, 80, 16, 0.3, 0.05),
