@@ -159,15 +159,15 @@ def blocks(lines):
 
 # ---- main program ---------------------------------------------------------------------------------------
 def dma(lines, slot):
-    """This wave's quarter (1 KiB) of the row at S_SRC into ring slot `slot` (LDS-DMA: M0 = wave-uniform LDS
-    base, lane l writes base + 16 l; one wait state after the M0 write)."""
+    """This wave's share (4 / WAVES KiB) of the row at S_SRC into ring slot `slot`, 1 KiB per LDS-DMA
+    instruction (M0 = wave-uniform LDS base, lane l writes base + 16 l; one wait state after the M0 write)."""
     if "novm" in DIAG:
         return
-    lines += [
-        f"s_add_u32 m0, s{S_LDSW}, {slot * 4096}",
-        "s_nop 0",
-        f"global_load_lds_dwordx4 %[dmaoff], s[{S_SRC}:{S_SRC + 1}]",
-    ]
+    # the instruction offset applies to the global AND the LDS address (LDS = M0 + offset + 16 lane)
+    lines += [f"s_add_u32 m0, s{S_LDSW}, {slot * 4096}", "s_nop 0"]
+    for d in range(4 // WAVES):
+        off = f" offset:{d * 1024}" if d else ""
+        lines.append(f"global_load_lds_dwordx4 %[dmaoff], s[{S_SRC}:{S_SRC + 1}]{off}")
 
 
 def advance(lines):
@@ -183,7 +183,7 @@ def advance(lines):
 def body(L, slot):
     """Source row j (slot = j % 3): its chunk is in ring slot `slot`, its block offsets in S_OFF[slot]."""
     if "novm" not in DIAG and "novmw" not in DIAG:
-        L.append("s_waitcnt vmcnt(1)")  # this wave's DMA of row j done (row j+1's may stay in flight)
+        L.append(f"s_waitcnt vmcnt({4 // WAVES})")  # this wave's DMAs of row j done (row j+1's may stay in flight)
     if "nobar" not in DIAG:
         L.append("s_barrier")  # every wave's quarter of row j landed; every wave is done reading row j-1's slot
     L.append(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
@@ -230,11 +230,14 @@ def body(L, slot):
                   for g in range(2) for o in range(8)]
             continue
         L += [
+            f"s_cmp_le_u32 s{S_ROWS}, {i}",  # rows i.. of this wave are past n_out: skip their products
+            "s_cbranch_scc1 7f",
             f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}",
             f"s_add_u32 s{S_TGT}, s{S_BASE}, s{cur + i}",
             f"s_addc_u32 s{S_TGT + 1}, s{S_BASE + 1}, 0",
             f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]",
         ]
+    L.append("7:")
     L.append("s_set_gpr_idx_off" if "absinline" not in DIAG else "s_nop 0")
 
 
@@ -301,7 +304,7 @@ def program():
 
 
 def main():
-    global BLOCK_BYTES, ALIGN
+    global BLOCK_BYTES, ALIGN, WAVES, WG_ROWS, STREAM_J_BYTES
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "bitslice_jump.inc"))
     ap.add_argument("--diag", default="", help="comma list: novm, inline, absinline (timing diagnostics, wrong results)")
@@ -311,17 +314,19 @@ def main():
     DIAG.update(x for x in args.diag.split(",") if x)
     assert args.stride >= BLOCK_BYTES and args.stride % 4 == 0
     BLOCK_BYTES, ALIGN = args.stride, args.align
-    lines = program()
     clob_v = ", ".join(f'"v{r}"' for r in range(LAST_VGPR + 1))
     clob_s = ", ".join(f'"s{r}"' for r in range(FIRST_SGPR, LAST_SGPR + 1))
-    body_txt = "\\n\\t".join(lines)
     with open(args.out, "w") as f:
-        f.write("// GENERATED by gen_bsjump.py -- do not edit.  Inner program of gf_matmul_bsj_kernel (kernels.hip).\n")
+        f.write("// GENERATED by gen_bsjump.py -- do not edit.  Inner programs of gf_matmul_bsj_kernel<W> (kernels.hip),\n"
+                "// W = 1, 2, 4 waves per workgroup (8 W output rows per tile).\n")
         f.write(f"#define RLNC_BSJ_NT {NT}\n")
-        f.write(f"#define RLNC_BSJ_WAVES {WAVES}\n")
         f.write(f"#define RLNC_BSJ_SLOTS {SLOTS}\n")
         f.write(f"#define RLNC_BSJ_BLOCK_BYTES {BLOCK_BYTES}\n")
-        f.write(f'#define RLNC_BSJ_ASM "{body_txt}"\n')
+        for w in (1, 2, 4):
+            WAVES, WG_ROWS = w, NT * w
+            STREAM_J_BYTES = WG_ROWS * 4
+            body_txt = "\\n\\t".join(program())
+            f.write(f'#define RLNC_BSJ_ASM_W{w} "{body_txt}"\n')
         f.write(f"#define RLNC_BSJ_CLOBBER_V {clob_v}\n")
         f.write(f'#define RLNC_BSJ_CLOBBER_S {clob_s}, "m0", "scc", "memory"\n')
 

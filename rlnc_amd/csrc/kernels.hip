@@ -219,6 +219,86 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_perm_kernel(MatmulParams p
     copy_header(p, t);
 }
 
+// Streaming variant for few output rows (n_out <= 3: one coded piece per pass is HBM-bound, ~1 multiply-add
+// per source byte read): the perm kernel's arithmetic with PF source rows in flight per lane (it keeps one
+// row pair), loaded non-temporally (each source byte is read once).  Whole aligned 4 KiB blocks only.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld16_nt(const uint8_t *ptr) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(ptr));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <int NT, int PF>
+__global__ __launch_bounds__(kThreads) void gf_matmul_stream_kernel(MatmulParams p, int row_tiles, int col_blocks) {
+    __shared__ uint4 s_t01[kKC][NT];
+    __shared__ uint32_t s_t2[kKC][NT];
+    const Tile t = make_tile<NT>(p, row_tiles, col_blocks);
+    const uint8_t *in_base = p.in + int64_t(t.obj) * p.in_obj + t.col;
+    const uint8_t *coef_base = p.coef + int64_t(t.obj) * p.coef_obj + int64_t(t.row0) * p.coef_row;
+    uint32_t acc[NT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0u;
+    for (int j0 = 0; j0 < p.n_in; j0 += kKC) {
+        const int kc = min(kKC, p.n_in - j0);
+        if (j0) __syncthreads();
+        for (int e = threadIdx.x; e < kKC * NT; e += kThreads) {
+            const int i = e % NT, j = e / NT;
+            const uint8_t c = (i < t.rows_here && j < kc) ? coef_base[int64_t(i) * p.coef_row + j0 + j] : uint8_t(0);
+            const PermTable pt = make_perm_table(c);
+            s_t01[j][i] = make_uint4(pt.t0lo, pt.t0hi, pt.t1lo, pt.t1hi);
+            s_t2[j][i] = pt.t2;
+        }
+        __syncthreads();
+        const uint8_t *rowp = in_base + int64_t(j0) * p.in_row;
+        // rows past the chunk re-read its last row (in bounds, unconditional: the loads stay countable, so
+        // the compiler waits for the oldest one only instead of draining all PF)
+        uint4 buf[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) buf[u] = ld16_nt(rowp + int64_t(min(u, kc - 1)) * p.in_row);
+        for (int jb = 0; jb < kc; jb += PF) {
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                const int j = jb + u;
+                if (j >= kc) break;
+                const uint4 x = buf[u];
+#ifdef RLNC_STREAM_DRAIN  // A/B build: conditional prefetch (the compiler then drains all PF loads per group)
+                if (j + PF < kc) buf[u] = ld16_nt(rowp + int64_t(j + PF) * p.in_row);
+#else
+                buf[u] = ld16_nt(rowp + int64_t(min(j + PF, kc - 1)) * p.in_row);
+#endif
+                const Sel a = selectors(x);
+#pragma unroll
+                for (int i = 0; i < NT; ++i) {
+                    const uint4 ta = s_t01[j][i];
+                    const uint32_t ta2 = s_t2[j][i];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        acc[i][q] = xor3(xor3(acc[i][q], vperm(ta.y, ta.x, a.s0[q]), vperm(ta.w, ta.z, a.s1[q])),
+                                         vperm(ta2, ta2, a.s2[q]), 0u);
+                }
+            }
+        }
+    }
+    store_tile<NT, true>(p, t, acc);
+    copy_header(p, t);
+}
+
+template <int NT>
+hipError_t launch_stream(const MatmulParams &p, int64_t full, hipStream_t s) {
+    MatmulParams q = p;
+    q.width = full;
+    const int row_tiles = (p.n_out + NT - 1) / NT;
+    const int col_blocks = int(full / kColBlock);
+    const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
+    if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+#ifndef RLNC_STREAM_PF
+#define RLNC_STREAM_PF 2  // A/B of 2..16 rows in flight: profiles/r01_stream_pf_ab.txt
+#endif
+    hipLaunchKernelGGL((gf_matmul_stream_kernel<NT, RLNC_STREAM_PF>), dim3(unsigned(total)), dim3(kThreads), 0, s, q,
+                       row_tiles, col_blocks);
+    return hipGetLastError();
+}
+
 // Wide variant: each lane owns VW 16-byte slots per source row (slot v at column v·4 KiB inside an
 // (VW·4 KiB) block), so every table read from LDS — the measured bottleneck of the VW = 1 kernel (a build
 // that reads one table set per source row ran 2.2× faster) — feeds VW× more multiply-adds.  Full aligned
@@ -690,40 +770,41 @@ hipError_t launch_bs(const MatmulParams &p, hipStream_t s, void *scratch, size_t
 #include "bitslice_jump.inc"
 #endif
 
-constexpr int kBsjWaveRows = RLNC_BSJ_NT;                   // output rows per wave
-constexpr int kBsjRows = RLNC_BSJ_NT * RLNC_BSJ_WAVES;        // output rows per workgroup tile
-constexpr int kBsjColBlock = 4096;                            // 64 lanes × 64 B, shared by the 4 waves
-static_assert(RLNC_BSJ_WAVES * 64 == kThreads, "one wave per 8-row slice of the tile");
+constexpr int kBsjWaveRows = RLNC_BSJ_NT;  // output rows per wave; a workgroup of W waves = 8 W rows
+constexpr int kBsjColBlock = 4096;          // 64 lanes × 64 B, shared by the W waves
 
 // stream[obj][row tile][j][row in tile] = c · RLNC_BSJ_BLOCK_BYTES (c = 0 for rows past n_out)
 __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, int64_t coef_obj, int64_t coef_row,
-                                                         int n_out, int n_in, int row_tiles, uint32_t *stream) {
-    const int64_t per_obj = int64_t(row_tiles) * n_in * kBsjRows;
+                                                         int n_out, int n_in, int row_tiles, int tile_rows,
+                                                         uint32_t *stream) {
+    const int64_t per_obj = int64_t(row_tiles) * n_in * tile_rows;
     const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     const int obj = blockIdx.y;
     if (e >= per_obj) return;
-    const int i = int(e % kBsjRows);
-    const int j = int((e / kBsjRows) % n_in);
-    const int rt = int(e / (int64_t(kBsjRows) * n_in));
-    const int row = rt * kBsjRows + i;
+    const int i = int(e % tile_rows);
+    const int j = int((e / tile_rows) % n_in);
+    const int rt = int(e / (int64_t(tile_rows) * n_in));
+    const int row = rt * tile_rows + i;
     const uint32_t c = row < n_out ? coef[int64_t(obj) * coef_obj + int64_t(row) * coef_row + j] : 0u;
     stream[int64_t(obj) * per_obj + e] = c * uint32_t(RLNC_BSJ_BLOCK_BYTES);
 }
 
-__global__ __launch_bounds__(kThreads) void gf_matmul_bsj_kernel(MatmulParams p, const uint32_t *stream,
-                                                                 int row_tiles, int col_blocks) {
+template <int W>
+__global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const uint32_t *stream, int row_tiles,
+                                                               int col_blocks) {
+    constexpr int kTileRows = kBsjWaveRows * W;
     __shared__ __attribute__((aligned(16))) uint8_t ring[RLNC_BSJ_SLOTS * kBsjColBlock];
     int rt, cb, obj;
     decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
-    const int row0 = rt * kBsjRows;
-    const int rows = min(kBsjRows, p.n_out - row0);
-    if (p.hdr != nullptr && cb == 0) {
-        Tile t;
-        t.obj = obj;
-        t.cb = 0;
-        t.row0 = row0;
-        t.rows_here = rows;
-        copy_header(p, t);
+    const int row0 = rt * kTileRows;
+    const int rows = min(kTileRows, p.n_out - row0);
+    if (p.hdr != nullptr && cb == 0) {  // coded-piece header (encoder.rs:246-248), 64·W threads
+        const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
+        uint8_t *h = p.hdr + int64_t(obj) * p.hdr_obj + int64_t(row0) * p.hdr_row;
+        for (int e = threadIdx.x; e < rows * p.n_in; e += 64 * W) {
+            const int i = e / p.n_in, j = e % p.n_in;
+            h[int64_t(i) * p.hdr_row + j] = coef_base[int64_t(i) * p.coef_row + j];
+        }
     }
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -731,24 +812,30 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_bsj_kernel(MatmulParams p,
     const uint8_t *src = p.in + int64_t(obj) * p.in_obj + int64_t(cb) * kBsjColBlock;
     uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0 + kBsjWaveRows * w) * p.out_row +
                    int64_t(cb) * kBsjColBlock;
-    const uint32_t *idx = stream + (int64_t(obj) * row_tiles + rt) * p.n_in * kBsjRows + kBsjWaveRows * w;
-    // LDS byte address of the ring (address-space-3 pointer value)
+    const uint32_t *idx = stream + (int64_t(obj) * row_tiles + rt) * p.n_in * kTileRows + kBsjWaveRows * w;
     typedef __attribute__((address_space(3))) uint8_t lds_u8;
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)ring));  // addrspacecast
-    const uint32_t ldsw = __builtin_amdgcn_readfirstlane(ring_lds + 1024u * uint32_t(w));
+    constexpr uint32_t kShare = kBsjColBlock / W;  // bytes of each row a wave moves into the ring
+    const uint32_t ldsw = __builtin_amdgcn_readfirstlane(ring_lds + kShare * uint32_t(w));
     const uint32_t ldsr = ring_lds + 16u * lane;
-    const uint32_t dmaoff = 1024u * uint32_t(w) + 16u * lane;
+    const uint32_t dmaoff = kShare * uint32_t(w) + 16u * lane;
     const uint32_t off = 16u * lane;
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-    asm volatile(RLNC_BSJ_ASM
-                 :
-                 : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),
-                   [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw),
-                   [off] "v"(off), [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr)
-                 : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S);
+#define RLNC_BSJ_OPERANDS                                                                                            \
+    : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),                           \
+      [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw), [off] "v"(off), \
+      [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr)                                                                      \
+    : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S
+    if constexpr (W == 1) asm volatile(RLNC_BSJ_ASM_W1 : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 2) asm volatile(RLNC_BSJ_ASM_W2 : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 4) asm volatile(RLNC_BSJ_ASM_W4 : RLNC_BSJ_OPERANDS);
+#undef RLNC_BSJ_OPERANDS
 #pragma clang diagnostic pop
 }
+
+// waves per workgroup: 8 output rows each, at most 4 (a 32-row tile), no more than the rows need
+inline int bsj_waves(int n_out) { return n_out <= 8 ? 1 : n_out <= 16 ? 2 : 4; }
 
 // Whole 4 KiB column blocks of 16-byte-aligned operands; the ragged tail goes to the perm kernel.
 bool bsj_eligible(const MatmulParams &p, bool aligned) {
@@ -757,29 +844,38 @@ bool bsj_eligible(const MatmulParams &p, bool aligned) {
 }
 
 size_t bsj_scratch_bytes(const MatmulParams &p) {
-    const int64_t tiles = (p.n_out + kBsjRows - 1) / kBsjRows;
+    const int tile_rows = kBsjWaveRows * bsj_waves(p.n_out);
+    const int64_t tiles = (p.n_out + tile_rows - 1) / tile_rows;
     // + one source: the main loop loads the offsets of the source after the last one
-    return size_t(int64_t(p.n_obj) * tiles * p.n_in * kBsjRows * 4 + 256);
+    return size_t(int64_t(p.n_obj) * tiles * p.n_in * tile_rows * 4 + 256);
 }
 
 hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full) {
     full = (p.width / kBsjColBlock) * kBsjColBlock;
-    const int row_tiles = (p.n_out + kBsjRows - 1) / kBsjRows;
+    const int W = bsj_waves(p.n_out), tile_rows = kBsjWaveRows * W;
+    const int row_tiles = (p.n_out + tile_rows - 1) / tile_rows;
     const int col_blocks = int(full / kBsjColBlock);
     const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
     if (scratch == nullptr || scratch_bytes < bsj_scratch_bytes(p)) return hipErrorInvalidValue;
     if (total > 0x7FFFFFFFLL || p.n_obj > 65535) return hipErrorInvalidValue;
     uint32_t *stream = static_cast<uint32_t *>(scratch);
-    const int64_t per_obj = int64_t(row_tiles) * p.n_in * kBsjRows;
+    const int64_t per_obj = int64_t(row_tiles) * p.n_in * tile_rows;
     if ((per_obj + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
     hipLaunchKernelGGL(bsj_offset_kernel, dim3(unsigned((per_obj + 255) / 256), unsigned(p.n_obj)), dim3(256), 0, s,
-                       p.coef, p.coef_obj, p.coef_row, p.n_out, p.n_in, row_tiles, stream);
+                       p.coef, p.coef_obj, p.coef_row, p.n_out, p.n_in, row_tiles, tile_rows, stream);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     MatmulParams q = p;
     q.width = full;
-    hipLaunchKernelGGL(gf_matmul_bsj_kernel, dim3(unsigned(total)), dim3(kThreads), 0, s, q, stream, row_tiles,
-                       col_blocks);
+    if (W == 1)
+        hipLaunchKernelGGL(gf_matmul_bsj_kernel<1>, dim3(unsigned(total)), dim3(64), 0, s, q, stream, row_tiles,
+                           col_blocks);
+    else if (W == 2)
+        hipLaunchKernelGGL(gf_matmul_bsj_kernel<2>, dim3(unsigned(total)), dim3(128), 0, s, q, stream, row_tiles,
+                           col_blocks);
+    else
+        hipLaunchKernelGGL(gf_matmul_bsj_kernel<4>, dim3(unsigned(total)), dim3(256), 0, s, q, stream, row_tiles,
+                           col_blocks);
     return hipGetLastError();
 }
 
@@ -930,6 +1026,19 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
     if (p.n_out <= 0 || p.width <= 0 || p.n_obj <= 0) return hipSuccess;
     const bool aligned = matmul_aligned(p);
     if (p.n_in <= 0) return hipErrorInvalidValue;
+    if (v == MatmulVariant::BitSlicedJump && aligned && p.n_out <= 3 && p.width >= kColBlock) {
+        // one to three coded pieces per source pass: HBM-bound, streamed with deep prefetch
+        const int64_t full = (p.width / kColBlock) * kColBlock;
+        hipError_t e = p.n_out == 1 ? launch_stream<1>(p, full, s)
+                                    : p.n_out == 2 ? launch_stream<2>(p, full, s) : launch_stream<3>(p, full, s);
+        if (e != hipSuccess || full == p.width) return e;
+        MatmulParams t = p;
+        t.in = p.in + full;
+        t.out = p.out + full;
+        t.width = p.width - full;
+        t.hdr = nullptr;
+        return launch_matmul(t, s, MatmulVariant::Perm);
+    }
     if (v == MatmulVariant::BitSliced || v == MatmulVariant::BitSlicedJump) {
         const bool jump = v == MatmulVariant::BitSlicedJump;
         v = MatmulVariant::Perm;  // whatever the bit-sliced kernels do not cover

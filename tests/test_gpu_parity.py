@@ -65,7 +65,7 @@ def test_primitives(ctx, n, off):
 SHAPES = [(1, 1, 1, 1), (1, 3, 17, 1), (2, 2, 16, 2), (3, 5, 4095, 1), (4, 32, 4096, 2), (5, 33, 4097, 1),
           (8, 7, 100, 3), (16, 16, 8192, 1), (17, 31, 5000, 2), (32, 32, 12288, 1), (33, 64, 4096, 1),
           (64, 32, 4096 * 3 + 48, 1), (70, 65, 333, 2), (16, 32, 8192 * 2, 2), (24, 9, 8192 + 4096 + 16, 1),
-          (9, 40, 32768, 1)]
+          (9, 40, 32768, 1), (1, 32, 8192 + 16, 2), (2, 7, 4096, 1), (3, 33, 12288 + 48, 2), (1, 70, 4096 * 5, 1)]
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
