@@ -1062,6 +1062,9 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
         return launch_wide_split<16, 2>(p, s);
     }
     if (v == MatmulVariant::Wide || v == MatmulVariant::Wide4) v = MatmulVariant::Perm;
+    // narrow (< one 4 KiB column block, e.g. the ragged tail of a recode over k + L bytes): the work is the
+    // sources x rows chain of one block, so split the rows over many workgroups (2 rows each)
+    if (p.width < kColBlock && p.n_out > 2) return launch_nt<2>(p, s, v, aligned);
     if (p.n_out <= 1) return launch_nt<1>(p, s, v, aligned);
     if (p.n_out <= 2) return launch_nt<2>(p, s, v, aligned);
     if (p.n_out <= 4) return launch_nt<4>(p, s, v, aligned);
