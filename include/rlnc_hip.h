@@ -106,12 +106,14 @@ int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc);
  *   5 = bitsliced  bit-plane transpose + register-indexed XOR of plane combinations (full 16 KiB column
  *                  blocks of 16-byte-aligned operands with >= 4 output rows; the rest goes to perm)
  *   6 = bitsliced-jump  as 5, but each (row, source) is one call into a code block specialised for the
- *                  coefficient (16 v_bitop3_b32 XOR3s of plane combinations) -- the default
+ *                  coefficient (16 v_bitop3_b32 XOR3s of plane combinations)
+ *   7 = bitsliced-jump-shared  as 6; in 32-row tiles each of the 4 waves builds one quarter of every source
+ *                  row's plane combinations and the quarters are exchanged through LDS -- the default
  * max_tile_rows caps the output rows per launch/workgroup (0 = automatic, else 1/2/4/8/16/32). */
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows);
 /* Where rlnc_decode_batch runs the coefficient elimination: 0 = auto (device when it fits LDS, default),
  * 1 = host threads, 2 = device, 3 = device with the clean-state steps on LDS instead of registers, 4 = device
- * with the clean-state steps on one wave's registers (2 spreads the initial clean run over 4 waves when k <= 32).
+ * with the clean-state steps on one wave's registers (2 spreads the initial clean run over 4 waves when k <= 64).
  * All are exact replicas; the switch exists for A/B tests. */
 int rlnc_set_decode_path(rlnc_context *ctx, int path);
 

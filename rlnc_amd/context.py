@@ -51,10 +51,11 @@ class Context:
         one wave's registers (all exact; 2-4 exist for A/B)."""
         check(self.lib.rlnc_set_decode_path(self.h, int(path)), self.lib)
 
-    def set_kernel_variant(self, variant: int = 6, max_tile_rows: int = 0):
-        """GF(2^8) matmul variant (include/rlnc_hip.h): 6 = bit-sliced, one code block per coefficient
-        (default), 5 = bit-sliced with register-indexed XORs, 0 = perm, 1 = nibble (the reference's 4-bit
-        tables, ablation), 2 = perm3, 3/4 = wide2/wide4.  All are bit-identical."""
+    def set_kernel_variant(self, variant: int = 7, max_tile_rows: int = 0):
+        """GF(2^8) matmul variant (include/rlnc_hip.h): 7 = bit-sliced, one code block per coefficient, plane
+        combinations built once per workgroup and shared through LDS (default), 6 = the same without sharing,
+        5 = bit-sliced with register-indexed XORs, 0 = perm, 1 = nibble (the reference's 4-bit tables,
+        ablation), 2 = perm3, 3/4 = wide2/wide4.  All are bit-identical."""
         check(self.lib.rlnc_set_kernel_variant(self.h, int(variant), int(max_tile_rows)), self.lib)
 
 

@@ -102,7 +102,7 @@ struct rlnc_context {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
-    rlnc::MatmulVariant variant = rlnc::MatmulVariant::BitSlicedJump;
+    rlnc::MatmulVariant variant = rlnc::MatmulVariant::BitSlicedJumpShared;
     int max_tile_rows = 0;
     int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination,
                           // 3 device elimination with the clean state on LDS, 4 ... on one wave's
@@ -331,7 +331,7 @@ int rlnc_set_decode_path(rlnc_context *ctx, int path) {
 
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows) {
     CHECK_ARG(ctx != nullptr);
-    CHECK_ARG(variant >= 0 && variant <= 6);
+    CHECK_ARG(variant >= 0 && variant <= 7);
     CHECK_ARG(max_tile_rows == 0 || max_tile_rows == 1 || max_tile_rows == 2 || max_tile_rows == 4 ||
               max_tile_rows == 8 || max_tile_rows == 16 || max_tile_rows == 32);
     ctx->variant = static_cast<rlnc::MatmulVariant>(variant);

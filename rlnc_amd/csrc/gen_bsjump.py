@@ -26,6 +26,16 @@ tile; one lane = 64 bytes as two 32-byte groups):
   * the block offsets c * BLOCK_BYTES of all (row, source) pairs come from the prep kernel's stream
     (s_load_dwordx8 per source, one source ahead); source rows are loaded two ahead into two staging buffers;
   * after all sources, the accumulators are transposed back and stored.
+A call is 4 scalar instructions (M0, low address half, s_swappc_b64, the block's s_setpc_b64): the high half
+is preset once the prologue has checked that the block table does not straddle a 4 GiB line (else the loop
+copy with the carry runs), and rows past n_out have c = 0, whose block returns at once.
+
+Shared-combination program (RLNC_BSJ_ASM_W4S, variant 7): with 4 waves on one column block, wave w builds
+only set w = (group w >> 1, half w & 1) of the plane combinations -- half of one group's transpose + 11 XORs
+instead of two full transposes + 44 XORs -- and the four sets (4 KiB each) are exchanged through two 16 KiB
+LDS slots.  Per source row j: barrier; 16 ds_read_b128 of row j's sets; the staging read of row j + 2 (the
+wave's group only); the DMA of row j + 4; the own set of row j + 1 (hides the set reads' latency); row j's
+calls.  Cost attribution (profiles/r01_bsj_diag.txt): calls ~10 %, the barrier ~7 %, the own set ~9 %.
 Run `python3 gen_bsjump.py` after editing; the output is committed.
 """
 import argparse
@@ -62,6 +72,20 @@ S_INROW, S_OUTROW, S_CNT, S_ROWS, S_T0, S_LDSW = 72, 73, 74, 75, 76, 77
 FIRST_SGPR, LAST_SGPR = S_OFF[0], S_LDSW
 BFI = "0xca"  # v_bitop3_b32 truth table of S0 ? S1 : S2 (index = S0 S1 S2)
 
+# shared-combination program (W = 4, gen --share): wave w builds only set w = (group w >> 1, half w & 1) of
+# the next source row and exchanges the four sets through LDS (two 16 KiB set slots)
+def RB(x, d):  # source-row staging buffer x (rows alternate), the wave's group only: 8 dwords
+    return 192 + 8 * x + d
+
+
+def OWN(x):  # the wave's own set of the next row, built here and written to LDS (OWN(0) = 0)
+    return 228 + x
+
+
+S_NDMA, S_H = 78, 79  # source rows still to advance over; the wave's half h
+CS_SLOT, CS_SET = 16384, 4096
+LAST_VGPR_ALL, LAST_SGPR_ALL = 243, S_H
+
 DIAG = set()
 ALIGN = 0  # log2 alignment of the first block (--align)
 
@@ -86,35 +110,44 @@ SHIFT_PAIRS = {0: ([(1, 3), (5, 7)], [(0, 2), (4, 6)]), 1: ([(2, 3), (6, 7)], [(
                2: ([(4, 5), (6, 7)], [(0, 1), (2, 3)])}
 
 
-def stage(k, cur, out, lines):
+def stage(k, cur, out, lines, need=range(8)):
+    """Outputs `need` (logical indices) of stage k; only the shifts those outputs read are issued."""
     s = 1 << k
+    need = set(need)
     left, right = SHIFT_PAIRS[k]
+    used_shl = {a + s for a in need if not (a >> k) & 1}  # output a (bit k clear) reads b << s, b = a + s
+    used_shr = {b - s for b in need if (b >> k) & 1}  # output b (bit k set) reads a >> s, a = b - s
     shl, shr = {}, {}
     t = TMP0
-    for pairs, op, dst in ((left, "v_lshlrev_b64", shl), (right, "v_lshrrev_b64", shr)):
+    for pairs, op, dst, used in ((left, "v_lshlrev_b64", shl, used_shl), (right, "v_lshrrev_b64", shr, used_shr)):
         for x, y in pairs:
+            if not {x, y} & used:
+                continue
             assert cur[y] == cur[x] + 1 and cur[x] % 2 == 0, (k, x, y, cur)
             lines.append(f"{op} v[{t}:{t + 1}], {s}, v[{cur[x]}:{cur[y]}]")
             dst[x], dst[y] = t, t + 1
             t += 2
-    assert not set(cur.values()) & set(out.values())
+    assert not {cur[a] for a in cur} & {out[a] for a in need}
     for a in range(8):
         if (a >> k) & 1:
             continue
         b = a + s
-        lines.append(f"v_bitop3_b32 {v(out[a])}, v{V_MASK[k]}, v{shl[b]}, {v(cur[a])} bitop3:{BFI}")  # m ? b<<s : a
-        lines.append(f"v_bitop3_b32 {v(out[b])}, v{V_MASK[k]}, {v(cur[b])}, v{shr[a]} bitop3:{BFI}")  # m ? b : a>>s
+        if a in need:
+            lines.append(f"v_bitop3_b32 {v(out[a])}, v{V_MASK[k]}, v{shl[b]}, {v(cur[a])} bitop3:{BFI}")  # m ? b<<s : a
+        if b in need:
+            lines.append(f"v_bitop3_b32 {v(out[b])}, v{V_MASK[k]}, {v(cur[b])}, v{shr[a]} bitop3:{BFI}")  # m ? b : a>>s
 
 
-def transpose(src, dst, lines):
+def transpose(src, dst, lines, half=None):
     """src: natural order (logical r in src[r], aligned consecutive registers); dst: any layout, disjoint
-    from src and X."""
+    from src and X.  half = h: only planes 4h..4h+3 (stage 1 in full, stages 2 and 0 on half the outputs)."""
     X = {r: V_X + r for r in range(8)}
     regs = [src[r] for r in range(8)]
     mid = {PHYS0[d]: regs[d] for d in range(8)}
+    need = range(8) if half is None else range(4 * half, 4 * half + 4)
     stage(1, src, X, lines)
-    stage(2, X, mid, lines)
-    stage(0, mid, dst, lines)
+    stage(2, X, mid, lines, need)
+    stage(0, mid, dst, lines, need)
 
 
 def combos(g, h, lines):
@@ -144,6 +177,10 @@ def block_indices(c):
 def blocks(lines):
     for c in range(256):
         lo, hi = block_indices(c)
+        if c == 0:  # no products (and the rows past n_out): return at once
+            lines.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+            lines += ["s_nop 0"] * ((BLOCK_BYTES - 4) // 4)
+            continue
         for g in range(2):
             for o in range(8):
                 a = ACC(0, g, o)
@@ -158,6 +195,39 @@ def blocks(lines):
 
 
 # ---- main program ---------------------------------------------------------------------------------------
+FAST = True  # the loop being generated: True = high half of every block address preset (no carry, checked)
+
+
+def call(L, cur, i):
+    """Row i's product of the current source: M0 = its accumulator slot, then the call into block c (whose
+    offset c * BLOCK_BYTES is s[cur + i]).  Rows past n_out have c = 0, whose block returns at once.  The fast
+    loop adds the low half only: the prologue has checked that the block table does not cross a 4 GiB line."""
+    L += [f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}", f"s_add_u32 s{S_TGT}, s{S_BASE}, s{cur + i}"]
+    if not FAST:
+        L.append(f"s_addc_u32 s{S_TGT + 1}, s{S_BASE + 1}, 0")
+    L.append(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
+
+
+def loops(L, body_fn, unroll):
+    """The main loop twice: fast (high address half preset) and, for a block table straddling a 4 GiB line,
+    with the carry; both leave through 3:."""
+    global FAST
+    L += [f"s_add_u32 s{S_T0}, s{S_BASE}, {256 * BLOCK_BYTES}",
+          "s_cbranch_scc1 12f" if "safe" not in DIAG else "s_branch 12f",  # --diag=safe: test the carry loop
+          f"s_mov_b32 s{S_TGT + 1}, s{S_BASE + 1}"]
+    for fast, top in ((True, 1), (False, 11)):
+        FAST = fast
+        L.append(f"{top}:" if fast else "12:")
+        if not fast:
+            L.append(f"{top}:")
+        for j in range(unroll):
+            body_fn(L, j)
+            L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f" if j < unroll - 1 else f"s_cbranch_scc0 {top}b"]
+        if fast:
+            L.append("s_branch 3f")
+    FAST = True
+    L += ["3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
+
 def dma(lines, slot):
     """This wave's share (4 / WAVES KiB) of the row at S_SRC into ring slot `slot`, 1 KiB per LDS-DMA
     instruction (M0 = wave-uniform LDS base, lane l writes base + 16 l; one wait state after the M0 write)."""
@@ -229,16 +299,125 @@ def body(L, slot):
             L += [f"v_bitop3_b32 v{ACC(i, g, o)}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])}, v{ACC(i, g, o)} bitop3:0x96"
                   for g in range(2) for o in range(8)]
             continue
-        L += [
-            f"s_cmp_le_u32 s{S_ROWS}, {i}",  # rows i.. of this wave are past n_out: skip their products
-            "s_cbranch_scc1 7f",
-            f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}",
-            f"s_add_u32 s{S_TGT}, s{S_BASE}, s{cur + i}",
-            f"s_addc_u32 s{S_TGT + 1}, s{S_BASE + 1}, 0",
-            f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]",
-        ]
-    L.append("7:")
+        call(L, cur, i)
     L.append("s_set_gpr_idx_off" if "absinline" not in DIAG else "s_nop 0")
+
+
+def advance_s(L):
+    """S_SRC -> the next source row while one is left (S_NDMA counts them down; SCC is read twice)."""
+    L += [
+        f"s_cmp_gt_u32 s{S_NDMA}, 0",
+        f"s_cselect_b32 s{S_T0}, s{S_INROW}, 0",
+        f"s_cselect_b32 s{S_TGT}, 1, 0",
+        f"s_sub_u32 s{S_NDMA}, s{S_NDMA}, s{S_TGT}",
+        f"s_add_u32 s{S_SRC}, s{S_SRC}, s{S_T0}",
+        f"s_addc_u32 s{S_SRC + 1}, s{S_SRC + 1}, 0",
+    ]
+
+
+def own_set(L, rb, cslot):
+    """Set (g, h) of the row staged in RB[rb]: planes 4h..4h+3 by the half transpose, the 11 composite
+    entries by VOP2 XORs, then 4 ds_write_b128 to set slot `cslot` (entry 0 is the zero register)."""
+    L += [f"s_cmp_eq_u32 s{S_H}, 0", "s_cbranch_scc0 4f"]
+    for h in range(2):
+        planes = {4 * h + b: OWN(1 << b) for b in range(4)}
+        transpose({d: RB(rb, d) for d in range(8)}, planes, L, half=h)
+        L += [f"v_xor_b32 v{OWN(x)}, v{OWN(y)}, v{OWN(z)}" for x, y, z in
+              [(3, 1, 2), (5, 1, 4), (6, 2, 4), (7, 3, 4), (9, 1, 8), (10, 2, 8), (11, 3, 8), (12, 4, 8),
+               (13, 5, 8), (14, 6, 8), (15, 7, 8)]]
+        L.append("s_branch 6f" if h == 0 else "6:")
+        if h == 0:
+            L.append("4:")
+    for q in range(4):
+        L.append(f"ds_write_b128 %[ldscw], v[{OWN(4 * q)}:{OWN(4 * q) + 3}] offset:{cslot * CS_SLOT + q * 1024}")
+
+
+def body_s(L, j):
+    """Source row j (j = the row index mod 6): sets of row j from LDS, row j + 2's staging read, row j + 4's
+    DMA, the own set of row j + 1, then row j's products."""
+    L += ["s_waitcnt vmcnt(1) lgkmcnt(0)",  # row j+2's DMA landed (row j+3's may fly); own set j + RB[j+1] done
+          "s_barrier" if "snobar" not in DIAG else "s_nop 0",  # every wave's set of row j written, row j+2
+          f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1"]                   # landed, row j+1's ring slot read by all
+    for st in range(4):
+        for q in range(4):
+            r = G(st >> 1, st & 1, 4 * q)
+            L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsc] offset:{(j % 2) * CS_SLOT + st * CS_SET + q * 1024}")
+    for hh in range(2):
+        r = RB(j % 2, 4 * hh)
+        L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{((j + 2) % SLOTS) * 4096 + hh * 1024}")
+    advance_s(L)
+    L += [f"s_add_u32 m0, s{S_LDSW}, {((j + 1) % SLOTS) * 4096}", "s_nop 0",
+          "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)]  # row j+4
+    if "snoown" in DIAG:  # timing only: the set writes without building the set
+        L += [f"ds_write_b128 %[ldscw], v[{OWN(4 * q)}:{OWN(4 * q) + 3}] offset:{((j + 1) % 2) * CS_SLOT + q * 1024}"
+              for q in range(4)]
+    else:
+        own_set(L, (j + 1) % 2, (j + 1) % 2)
+    cur, nxt = S_OFF[j % 3], S_OFF[(j + 1) % 3]
+    L += [
+        # the 16 set reads (LDS returns in order; 2 staging reads + 4 writes may fly)
+        "s_waitcnt lgkmcnt(6)" if "snowait" not in DIAG else "s_nop 0",
+        f"s_load_dwordx8 s[{nxt}:{nxt + 7}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
+        f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
+        f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
+        "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)",
+    ]
+    for i in range(NT):
+        if "sinline" in DIAG:  # timing only: a fixed coefficient's products inline (relative), no call
+            L.append(f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}")
+            lo, hi = block_indices(0x53 + i)
+            L += [f"v_bitop3_b32 v{ACC(0, g, o)}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])}, v{ACC(0, g, o)} bitop3:0x96"
+                  for g in range(2) for o in range(8)]
+            continue
+        call(L, cur, i)
+    L.append("s_set_gpr_idx_off")
+
+
+def program_shared():
+    assert WAVES == 4
+    L = [
+        f"s_mov_b64 s[{S_SRC}:{S_SRC + 1}], %[src]",
+        f"s_mov_b64 s[{S_IDX}:{S_IDX + 1}], %[idx]",
+        f"s_mov_b64 s[{S_DST}:{S_DST + 1}], %[dst]",
+        f"s_mov_b32 s{S_INROW}, %[in_row]",
+        f"s_mov_b32 s{S_OUTROW}, %[out_row]",
+        f"s_mov_b32 s{S_CNT}, %[n_in]",
+        f"s_sub_u32 s{S_NDMA}, %[n_in], 1",
+        f"s_mov_b32 s{S_H}, %[half]",
+        f"s_mov_b32 s{S_ROWS}, %[rows]",
+        f"v_mov_b32 v{V_MASK[0]}, 0xaaaaaaaa",
+        f"v_mov_b32 v{V_MASK[1]}, 0xcccccccc",
+        f"v_mov_b32 v{V_MASK[2]}, 0xf0f0f0f0",
+        f"s_getpc_b64 s[{S_BASE}:{S_BASE + 1}]",
+        "5:",
+        f"s_add_u32 s{S_BASE}, s{S_BASE}, (9f - 5b)",
+        f"s_addc_u32 s{S_BASE + 1}, s{S_BASE + 1}, 0",
+        f"s_mov_b32 s{S_LDSW}, %[ldsw]",
+    ]
+    dmai = "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)
+    for slot in range(3):  # rows 0, 1, 2 (clamped to the last row) into ring slots 0, 1, 2
+        if slot:
+            advance_s(L)
+        L += [f"s_add_u32 m0, s{S_LDSW}, {slot * 4096}", "s_nop 0", dmai]
+    L.append(f"s_load_dwordx8 s[{S_OFF[0]}:{S_OFF[0] + 7}], s[{S_IDX}:{S_IDX + 1}], 0")
+    L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
+    L.append(f"v_mov_b32 v{OWN(0)}, 0")
+    L += ["s_waitcnt vmcnt(1)", "s_barrier"]  # rows 0 and 1 landed (all waves)
+    for x in range(2):
+        for hh in range(2):
+            r = RB(x, 4 * hh)
+            L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{x * 4096 + hh * 1024}")
+    L += ["s_waitcnt lgkmcnt(0)", "s_barrier"]  # every wave has read slot 0: row 3 may overwrite it
+    advance_s(L)
+    L += [f"s_add_u32 m0, s{S_LDSW}, 0", "s_nop 0", dmai]
+    own_set(L, 0, 0)  # row 0's own set into set slot 0
+    loops(L, body_s, 6)
+    epilogue(L)
+    L.append("s_branch 8f")
+    L.append("9:")
+    blocks(L)
+    L.append("8:")
+    return L
 
 
 def epilogue(L):
@@ -286,13 +465,7 @@ def program():
     L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
     L += [f"v_mov_b32 {v(G(g, h, 0))}, 0" for g in range(2) for h in range(2)]
     # loop over source rows j, three per trip (ring slot and offset buffer j % 3 are immediates)
-    L.append("1:")
-    body(L, 0)
-    L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f"]
-    body(L, 1)
-    L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f"]
-    body(L, 2)
-    L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc0 1b", "3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    loops(L, body, 3)
     epilogue(L)
     L.append("s_branch 8f")
     if ALIGN:
@@ -314,8 +487,8 @@ def main():
     DIAG.update(x for x in args.diag.split(",") if x)
     assert args.stride >= BLOCK_BYTES and args.stride % 4 == 0
     BLOCK_BYTES, ALIGN = args.stride, args.align
-    clob_v = ", ".join(f'"v{r}"' for r in range(LAST_VGPR + 1))
-    clob_s = ", ".join(f'"s{r}"' for r in range(FIRST_SGPR, LAST_SGPR + 1))
+    clob_v = ", ".join(f'"v{r}"' for r in range(LAST_VGPR_ALL + 1))
+    clob_s = ", ".join(f'"s{r}"' for r in range(FIRST_SGPR, LAST_SGPR_ALL + 1))
     with open(args.out, "w") as f:
         f.write("// GENERATED by gen_bsjump.py -- do not edit.  Inner programs of gf_matmul_bsj_kernel<W> (kernels.hip),\n"
                 "// W = 1, 2, 4 waves per workgroup (8 W output rows per tile).\n")
@@ -327,6 +500,11 @@ def main():
             STREAM_J_BYTES = WG_ROWS * 4
             body_txt = "\\n\\t".join(program())
             f.write(f'#define RLNC_BSJ_ASM_W{w} "{body_txt}"\n')
+        WAVES, WG_ROWS = 4, NT * 4
+        STREAM_J_BYTES = WG_ROWS * 4
+        body_txt = "\\n\\t".join(program_shared())
+        f.write(f'#define RLNC_BSJ_ASM_W4S "{body_txt}"\n')
+        f.write(f"#define RLNC_BSJ_CSET_BYTES {2 * CS_SLOT}\n")
         f.write(f"#define RLNC_BSJ_CLOBBER_V {clob_v}\n")
         f.write(f'#define RLNC_BSJ_CLOBBER_S {clob_s}, "m0", "scc", "memory"\n')
 

@@ -789,11 +789,15 @@ __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, in
     stream[int64_t(obj) * per_obj + e] = c * uint32_t(RLNC_BSJ_BLOCK_BYTES);
 }
 
-template <int W>
+// SHARE (W = 4 only): wave w builds one of the four combination sets of each source row and the sets are
+// exchanged through LDS (RLNC_BSJ_ASM_W4S) instead of every wave building all four
+template <int W, bool SHARE = false>
 __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const uint32_t *stream, int row_tiles,
                                                                int col_blocks) {
+    static_assert(!SHARE || W == 4, "the shared-set program is generated for 4 waves");
     constexpr int kTileRows = kBsjWaveRows * W;
     __shared__ __attribute__((aligned(16))) uint8_t ring[RLNC_BSJ_SLOTS * kBsjColBlock];
+    __shared__ __attribute__((aligned(16))) uint8_t cset[SHARE ? RLNC_BSJ_CSET_BYTES : 16];
     int rt, cb, obj;
     decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
     const int row0 = rt * kTileRows;
@@ -820,16 +824,22 @@ __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, c
     const uint32_t ldsr = ring_lds + 16u * lane;
     const uint32_t dmaoff = kShare * uint32_t(w) + 16u * lane;
     const uint32_t off = 16u * lane;
+    const uint32_t ldsc = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)cset)) + 16u * lane;
+    const uint32_t ldscw = ldsc + 4096u * uint32_t(w);      // this wave's set (group w >> 1, half w & 1)
+    const uint32_t ldsrg = ldsr + 2048u * uint32_t(w >> 1);  // this wave's group of the ring chunk
+    const uint32_t half = uint32_t(w & 1);
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
 #define RLNC_BSJ_OPERANDS                                                                                            \
     : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),                           \
       [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw), [off] "v"(off), \
-      [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr)                                                                      \
+      [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr), [ldsc] "v"(ldsc), [ldscw] "v"(ldscw), [ldsrg] "v"(ldsrg),           \
+      [half] "s"(half)                                                                                            \
     : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S
     if constexpr (W == 1) asm volatile(RLNC_BSJ_ASM_W1 : RLNC_BSJ_OPERANDS);
     if constexpr (W == 2) asm volatile(RLNC_BSJ_ASM_W2 : RLNC_BSJ_OPERANDS);
-    if constexpr (W == 4) asm volatile(RLNC_BSJ_ASM_W4 : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 4 && !SHARE) asm volatile(RLNC_BSJ_ASM_W4 : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 4 && SHARE) asm volatile(RLNC_BSJ_ASM_W4S : RLNC_BSJ_OPERANDS);
 #undef RLNC_BSJ_OPERANDS
 #pragma clang diagnostic pop
 }
@@ -850,7 +860,8 @@ size_t bsj_scratch_bytes(const MatmulParams &p) {
     return size_t(int64_t(p.n_obj) * tiles * p.n_in * tile_rows * 4 + 256);
 }
 
-hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full) {
+hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full,
+                      bool share) {
     full = (p.width / kBsjColBlock) * kBsjColBlock;
     const int W = bsj_waves(p.n_out), tile_rows = kBsjWaveRows * W;
     const int row_tiles = (p.n_out + tile_rows - 1) / tile_rows;
@@ -873,6 +884,9 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
     else if (W == 2)
         hipLaunchKernelGGL(gf_matmul_bsj_kernel<2>, dim3(unsigned(total)), dim3(128), 0, s, q, stream, row_tiles,
                            col_blocks);
+    else if (share)
+        hipLaunchKernelGGL((gf_matmul_bsj_kernel<4, true>), dim3(unsigned(total)), dim3(256), 0, s, q, stream,
+                           row_tiles, col_blocks);
     else
         hipLaunchKernelGGL(gf_matmul_bsj_kernel<4>, dim3(unsigned(total)), dim3(256), 0, s, q, stream, row_tiles,
                            col_blocks);
@@ -1015,8 +1029,8 @@ static bool matmul_aligned(const MatmulParams &p) {
 }
 
 size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v) {
-    if ((v != MatmulVariant::BitSliced && v != MatmulVariant::BitSlicedJump) || p.n_out <= 0 || p.n_in <= 0 ||
-        p.n_obj <= 0)
+    if ((v != MatmulVariant::BitSliced && v != MatmulVariant::BitSlicedJump && v != MatmulVariant::BitSlicedJumpShared) ||
+        p.n_out <= 0 || p.n_in <= 0 || p.n_obj <= 0)
         return 0;
     if (v == MatmulVariant::BitSliced) return bs_eligible(p, matmul_aligned(p)) ? bs_scratch_bytes(p) : 0;
     return bsj_eligible(p, matmul_aligned(p)) ? bsj_scratch_bytes(p) : 0;
@@ -1026,7 +1040,8 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
     if (p.n_out <= 0 || p.width <= 0 || p.n_obj <= 0) return hipSuccess;
     const bool aligned = matmul_aligned(p);
     if (p.n_in <= 0) return hipErrorInvalidValue;
-    if (v == MatmulVariant::BitSlicedJump && aligned && p.n_out <= 3 && p.width >= kColBlock) {
+    const bool jump = v == MatmulVariant::BitSlicedJump || v == MatmulVariant::BitSlicedJumpShared;
+    if (jump && aligned && p.n_out <= 3 && p.width >= kColBlock) {
         // one to three coded pieces per source pass: HBM-bound, streamed with deep prefetch
         const int64_t full = (p.width / kColBlock) * kColBlock;
         hipError_t e = p.n_out == 1 ? launch_stream<1>(p, full, s)
@@ -1039,12 +1054,12 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
         t.hdr = nullptr;
         return launch_matmul(t, s, MatmulVariant::Perm);
     }
-    if (v == MatmulVariant::BitSliced || v == MatmulVariant::BitSlicedJump) {
-        const bool jump = v == MatmulVariant::BitSlicedJump;
+    if (v == MatmulVariant::BitSliced || jump) {
+        const bool share = v == MatmulVariant::BitSlicedJumpShared;
         v = MatmulVariant::Perm;  // whatever the bit-sliced kernels do not cover
         if (jump ? bsj_eligible(p, aligned) : bs_eligible(p, aligned)) {
             int64_t full = 0;
-            hipError_t e = jump ? launch_bsj(p, s, scratch, scratch_bytes, full)
+            hipError_t e = jump ? launch_bsj(p, s, scratch, scratch_bytes, full, share)
                                 : launch_bs(p, s, scratch, scratch_bytes, full);
             if (e != hipSuccess || full == p.width) return e;
             MatmulParams t = p;

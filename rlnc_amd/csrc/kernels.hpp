@@ -35,7 +35,8 @@ enum class MatmulVariant : int {
     Wide = 3,
     Wide4 = 4,
     BitSliced = 5,
-    BitSlicedJump = 6
+    BitSlicedJump = 6,
+    BitSlicedJumpShared = 7  // 6 with each row's combination sets built once per workgroup (4-wave tiles)
 };
 
 // Device scratch the BitSliced variant needs for its coefficient-index stream (0 for the others, and for

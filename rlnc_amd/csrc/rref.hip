@@ -550,23 +550,25 @@ __device__ int reg_run(const Mat &M, const uint32_t *tab, uint32_t (&v)[RT], con
 // work per piece is 1/NW of the single-wave path's.  Returns the next piece index; on exit (all pieces done,
 // or a kept row with a zero diagonal ends the clean state) the whole matrix is in LDS.
 // ---------------------------------------------------------------------------------------------------
-template <int NW>
+template <int NW, int MG, int RTW>
 __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, uint32_t *P, int m, int k, int &rows,
                           bool &clean, int32_t *St) {
-    constexpr int G = 4, DP = 16, RTW = 2;
+    constexpr int G = MG, DP = 64 / MG;
+    constexpr bool kPre = RTW <= 8;  // few rows per lane: the next piece's forward tables are prefetched
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int w = lane % DP, g = lane / DP;
     const bool wl = w < M.D;
     uint32_t cm = 0;  // coefficient bytes (< k) of this lane's dword
     if (wl && 4 * w < k) cm = 4 * w + 4 <= k ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (8 * (4 * w + 4 - k)));
-    uint32_t v[RTW] = {0u, 0u};
-    auto row_of = [&](int t) { return 8 * wave + G * t + g; };
-    // forward operands of piece pc for row count r: init dword w and the tables of M[r][i] for own rows i
-    uint32_t init = 0, t2[RTW];
-    uint4 t4[RTW];
+    uint32_t v[RTW];
+#pragma unroll
+    for (int t = 0; t < RTW; ++t) v[t] = 0;
+    auto row_of = [&](int t) { return RTW * G * wave + G * t + g; };
+    // forward operands of piece pc for row count r: init dword w, quotients M[r][i] of own rows (and tables)
+    uint32_t init = 0, q[RTW], t2[kPre ? RTW : 1];
+    uint4 t4[kPre ? RTW : 1];
     auto load_ops = [&](int pc, int r) {
         const uint8_t *h = H + pc * k;
-        uint32_t q[RTW];
 #pragma unroll
         for (int t = 0; t < RTW; ++t) q[t] = row_of(t) < r ? uint32_t(h[row_of(t)]) : 0u;
         uint32_t x = 0;
@@ -578,10 +580,12 @@ __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, u
             }
         }
         init = x;
+        if constexpr (kPre) {
 #pragma unroll
-        for (int t = 0; t < RTW; ++t) {
-            t4[t] = *reinterpret_cast<const uint4 *>(tab + q[t] * kTabDw);
-            t2[t] = tab[q[t] * kTabDw + 4];
+            for (int t = 0; t < RTW; ++t) {
+                t4[t] = *reinterpret_cast<const uint4 *>(tab + q[t] * kTabDw);
+                t2[t] = tab[q[t] * kTabDw + 4];
+            }
         }
     };
     auto to_lds = [&](int nrows) {
@@ -598,10 +602,14 @@ __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, u
             continue;
         }
         uint32_t acc = 0;
+        if constexpr (kPre) {
 #pragma unroll
-        for (int t = 0; t < RTW; ++t) acc ^= mul4t(t4[t], t2[t], v[t]);
-        acc ^= __shfl_xor(acc, 16);
-        acc ^= __shfl_xor(acc, 32);
+            for (int t = 0; t < RTW; ++t) acc ^= mul4t(t4[t], t2[t], v[t]);
+        } else {
+            acc = dot_chunked<RTW>(tab, q, v);
+        }
+#pragma unroll
+        for (int sh = DP; sh < 64; sh <<= 1) acc ^= __shfl_xor(acc, sh);
         uint32_t *Pb = P + buf * NW * DP;
         if (lane < DP) Pb[wave * DP + lane] = acc;
         __syncthreads();
@@ -630,18 +638,22 @@ __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, u
         const uint32_t mask = from_mask(w, r + 1);
         nr = (nr & ~mask) | (mul4t(ti4, ti2, nr) & mask);
         if (w == rw) nr = (nr & ~(0xFFu << rb)) | (1u << rb);
-        uint4 b4[RTW];
-        uint32_t b2[RTW];
-#pragma unroll
-        for (int t = 0; t < RTW; ++t) {
-            const uint32_t qb = (__shfl(v[t], rw + DP * g) >> rb) & 0xFFu;  // M[row][r], row in this wave
-            b4[t] = *reinterpret_cast<const uint4 *>(tab + qb * kTabDw);
-            b2[t] = tab[qb * kTabDw + 4];
-        }
         rows = r + 1;
-        if (pc + 1 < m) load_ops(pc + 1, r + 1);
 #pragma unroll
-        for (int t = 0; t < RTW; ++t) v[t] ^= mul4t(b4[t], b2[t], nr);
+        for (int c0 = 0; c0 < RTW; c0 += 8) {  // backward in chunks of 8 rows (table reads issued together)
+            constexpr int U = RTW < 8 ? RTW : 8;
+            uint4 b4[U];
+            uint32_t b2[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t qb = (__shfl(v[c0 + u], rw + DP * g) >> rb) & 0xFFu;  // M[row][r], row in this wave
+                b4[u] = *reinterpret_cast<const uint4 *>(tab + qb * kTabDw);
+                b2[u] = tab[qb * kTabDw + 4];
+            }
+            if (c0 == 0 && pc + 1 < m) load_ops(pc + 1, r + 1);
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[c0 + u] ^= mul4t(b4[u], b2[u], nr);
+        }
 #pragma unroll
         for (int t = 0; t < RTW; ++t)
             if (row_of(t) == r) v[t] = nr;
@@ -655,7 +667,7 @@ __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, u
 // G > 0: the clean state runs on registers (reg_run<G, RT>); G = 0: on LDS (clean_append).  NW > 1: the
 // initial clean run is spread over NW waves (reg_run_mw); then waves 1..NW-1 end and wave 0 continues alone
 // (S_BARRIER waits only for the waves that have not terminated).
-template <int G, int RT, int NW>
+template <int G, int RT, int NW, int MG = 4, int MRTW = 2>
 __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, int hdr_lds) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;  // kTabEntries × kTabDw dwords
@@ -714,7 +726,7 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, in
     uint64_t prof_t = t_setup;
 #endif
     if constexpr (NW > 1) {
-        pc0 = reg_run_mw<NW>(M, tab, H, P, m, k, rows, clean, St);
+        pc0 = reg_run_mw<NW, MG, MRTW>(M, tab, H, P, m, k, rows, clean, St);
         if (threadIdx.x >= 64) return;  // wave 0 finishes alone (generic path / output)
 #ifdef RLNC_RREF_PROFILE  // diagnostic: slot 0 = setup cycles, slot 1 = the multi-wave clean run
         prof[0] = t_setup - t_start;
@@ -725,7 +737,7 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, in
     uint32_t v[G > 0 ? RT : 1];
 #pragma unroll
     for (int t = 0; t < (G > 0 ? RT : 1); ++t) v[t] = 0;
-    if constexpr (NW > 1)
+    if constexpr (NW > 1 && G > 0)
         if (clean && rows > 0 && pc0 < m) lds_to_regs<G, RT>(M, v, rows);
     for (int pc = pc0; pc < m; ++pc) {
         if constexpr (G > 0) {
@@ -792,9 +804,9 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, in
 size_t rref_lds_bytes(int k, int m) {
     return kTabEntries * kTabDw * 4 + size_t(k + 1) * 4 * size_t(rref_row_dwords(k, m)) + 4 * ((size_t(m) + 3) & ~size_t(3));
 }
-// + the staged headers, + 2 × 4 × 16 dwords of multi-wave partial sums
+// + the staged headers, + 2 × 4 × 64 dwords of multi-wave partial sums
 static size_t rref_lds_bytes_staged(int k, int m) {
-    return rref_lds_bytes(k, m) + ((size_t(k) * m + 15) & ~size_t(15)) + 2 * 4 * 16 * 4;
+    return rref_lds_bytes(k, m) + ((size_t(k) * m + 15) & ~size_t(15)) + 2 * 4 * 64 * 4;
 }
 
 hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
@@ -804,22 +816,23 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     const int hdr_lds = rref_lds_bytes_staged(p.k, p.m) <= kRrefMaxLds ? 1 : 0;
     if (hdr_lds) lds = rref_lds_bytes_staged(p.k, p.m);
     // register-resident clean path when the matrix fits: rows <= G·RT, row dwords <= 64 / G; the initial clean
-    // run spread over 4 waves when k <= 32 and rows are <= 16 dwords
+    // run spread over 4 waves (reg_run_mw) up to k = 64
     const int D = rref_row_dwords(p.k, p.m);
     auto kern = &gf_rref_batch_kernel<0, 1, 1>;
     int threads = 64;
     if (p.lds_only != 1 && hdr_lds) {  // the register paths read the staged headers
+        const bool mw = p.lds_only == 0;
         if (D <= 16 && p.k <= 32) {
-            kern = p.lds_only == 0 ? &gf_rref_batch_kernel<4, 8, 4> : &gf_rref_batch_kernel<4, 8, 1>;
-            threads = p.lds_only == 0 ? 256 : 64;
+            kern = mw ? &gf_rref_batch_kernel<4, 8, 4, 4, 2> : &gf_rref_batch_kernel<4, 8, 1>;
         } else if (D <= 32 && p.k <= 64) {
-            kern = &gf_rref_batch_kernel<2, 32, 1>;
-        }
+            kern = mw ? &gf_rref_batch_kernel<2, 32, 4, 2, 8> : &gf_rref_batch_kernel<2, 32, 1>;
+        }  // k = 128 (<0, 1, 4, 1, 32>: 3.8 ms for 512 objects) stays on the one-wave LDS path (2.5 ms)
+        if (mw && kern != &gf_rref_batch_kernel<0, 1, 1>) threads = 256;
     }
     static bool attr_set = false;
     if (!attr_set) {
-        for (auto f : {&gf_rref_batch_kernel<0, 1, 1>, &gf_rref_batch_kernel<4, 8, 1>, &gf_rref_batch_kernel<4, 8, 4>,
-                       &gf_rref_batch_kernel<2, 32, 1>}) {
+        for (auto f : {&gf_rref_batch_kernel<0, 1, 1>, &gf_rref_batch_kernel<4, 8, 1>, &gf_rref_batch_kernel<4, 8, 4, 4, 2>,
+                       &gf_rref_batch_kernel<2, 32, 1>, &gf_rref_batch_kernel<2, 32, 4, 2, 8>}) {
             hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(f),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, int(kRrefMaxLds));
             if (e != hipSuccess) return e;

@@ -12,7 +12,7 @@ from tests.gpu_util import MUL, dev, host, np_matmul
 
 pytestmark = pytest.mark.gpu
 
-DEFAULT_VARIANT = 6  # rlnc_context default (bit-sliced jump, perm for what it does not cover)
+DEFAULT_VARIANT = 7  # rlnc_context default (bit-sliced jump with shared combinations, perm for the rest)
 
 S = ["Ok", "CodingVectorLengthMismatch", "DataLengthMismatch", "PieceCountZero", "DataLengthZero",
      "PieceLengthZero", "NotEnoughPiecesToRecode", "PieceLengthTooShort", "PieceNotUseful", "ReceivedAllPieces",
@@ -68,7 +68,7 @@ SHAPES = [(1, 1, 1, 1), (1, 3, 17, 1), (2, 2, 16, 2), (3, 5, 4095, 1), (4, 32, 4
           (9, 40, 32768, 1), (1, 32, 8192 + 16, 2), (2, 7, 4096, 1), (3, 33, 12288 + 48, 2), (1, 70, 4096 * 5, 1)]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("n_out,n_in,W,nobj", SHAPES)
 def test_matmul(ctx, variant, n_out, n_in, W, nobj):
     from rlnc_amd import batch
@@ -97,7 +97,7 @@ BS_SHAPES = [(4, 1, 16384, 1), (5, 2, 16384 + 16, 2), (8, 32, 32768, 1), (9, 31,
              (3, 5, 16384, 1)]
 
 
-@pytest.mark.parametrize("variant", [5, 6])
+@pytest.mark.parametrize("variant", [5, 6, 7])
 @pytest.mark.parametrize("n_out,n_in,W,nobj", BS_SHAPES)
 def test_matmul_bitsliced(ctx, variant, n_out, n_in, W, nobj):
     from rlnc_amd import batch
@@ -119,7 +119,7 @@ def test_matmul_bitsliced(ctx, variant, n_out, n_in, W, nobj):
         assert np.array_equal(got[o], np_matmul(coef[o], inp[o])), o
 
 
-@pytest.mark.parametrize("variant", [5, 6])
+@pytest.mark.parametrize("variant", [5, 6, 7])
 def test_matmul_every_coefficient(ctx, variant):
     """All 256 coefficients (16 rows x 16 sources = 0..255) against every byte value: each of the jump
     variant's 256 code blocks, and every index pattern of the relative-XOR variant."""
@@ -139,7 +139,7 @@ def test_matmul_every_coefficient(ctx, variant):
     assert np.array_equal(got[0], np_matmul(coef[0], inp[0]))
 
 
-@pytest.mark.parametrize("variant", [5, 6])
+@pytest.mark.parametrize("variant", [5, 6, 7])
 def test_matmul_bitsliced_strided_with_header(ctx, variant):
     """Padded row strides and the coded-piece header copy, through the raw C ABI descriptor."""
     import ctypes as C
@@ -303,7 +303,8 @@ def _sequences(rng, nobj, k, m, L, sparsity, dep_frac):
 
 
 @pytest.mark.parametrize("path", [1, 2, 3, 4])
-@pytest.mark.parametrize("k,m,L,sparsity,dep", [(32, 32, 40, 0.0, 0.0), (64, 64, 24, 0.0, 0.1),
+@pytest.mark.parametrize("k,m,L,sparsity,dep", [(32, 32, 40, 0.0, 0.0), (64, 64, 24, 0.0, 0.1), (128, 128, 20, 0.0, 0.0),
+                                                (100, 120, 9, 0.0, 0.1), (120, 128, 16, 0.9, 0.02),
                                                 (48, 56, 10, 0.4, 0.1), (64, 70, 9, 0.85, 0.05), (8, 14, 5, 0.7, 0.1), (8, 12, 33, 0.9, 0.0), (32, 40, 64, 0.0, 0.2),
                                                 (32, 36, 16, 0.6, 0.1), (17, 30, 7, 0.5, 0.2), (70, 80, 16, 0.3, 0.05),
                                                 (1, 3, 4, 0.5, 0.0), (128, 130, 16, 0.0, 0.02),
