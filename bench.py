@@ -189,6 +189,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--encode-only", action="store_true", help="diagnostic: time only the encode launch")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1: the decoder's elimination (reads only the coded pieces' coefficient headers, written "
+                         "first) runs on a second stream while the encode's data work runs; 0: strictly serial")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay each step as one captured HIP graph (the kernels of a step, launched together)")
     args = ap.parse_args()
@@ -225,16 +228,50 @@ def main():
 
     enc_events = []
     dec_events = []
+    # pipelined step: the coded pieces' headers are written first (one strided copy), then the decoder's
+    # elimination — which reads nothing else — runs on a side stream (its own context) concurrently with the
+    # encode's data work; the data side of the decode waits for both.  Same kernels, same bytes as serial.
+    ctx_side = rlnc_amd.Context(dist.local_rank) if args.pipeline else None
+    side = torch.cuda.Stream(dev) if args.pipeline else None
+    ev_start, ev_elim = torch.cuda.Event(), torch.cuda.Event()
+    T = torch.empty((B, k, m), dtype=torch.uint8, device=dev)
+    rank = torch.empty(B, dtype=torch.int32, device=dev)
+
+    def encode_launches():
+        if args.pipeline:
+            # side stream: the coded pieces' headers (bytes 0..k of each piece), then the elimination over them;
+            # launch stream: the data bytes k.. of the same pieces (disjoint bytes), concurrently
+            ev_start.record()
+            with torch.cuda.stream(side):
+                side.wait_event(ev_start)
+                batch.encode_batch_headers(coeffs, pieces, ctx_side)
+                if not args.encode_only:
+                    batch.decode_batch_eliminate(received, k, T, piece_status, rank, ctx_side)
+                ev_elim.record()
+            batch.encode_batch_data(src, coeffs, pieces, ctx)
+            if args.encode_only:
+                torch.cuda.current_stream().wait_event(ev_elim)
+        else:
+            batch.encode_batch(src, coeffs, pieces, ctx)
+
+    def decode_launches():
+        if args.encode_only:
+            return
+        if args.pipeline:
+            torch.cuda.current_stream().wait_event(ev_elim)
+            batch.decode_batch_apply(received, k, T, rank, decoded, object_status, data_len, ctx)
+        else:
+            batch.decode_batch_device(received, k, decoded, piece_status, object_status, data_len, ctx)
 
     def step():
-        # encode launch, then the whole device-side decode (elimination + T×data + marker scan), all
-        # asynchronous on torch's current stream; HIP events bracket each on that stream
+        # encode, then the device-side decode (elimination + T×data + marker scan), asynchronous; HIP events
+        # on the launch stream bracket each part (pipelined: the encode part includes the concurrent elimination's
+        # interference, the decode part any wait for it)
         e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         e0.record()
-        batch.encode_batch(src, coeffs, pieces, ctx)
+        encode_launches()
         e1.record()
-        if not args.encode_only:
-            batch.decode_batch_device(received, k, decoded, piece_status, object_status, data_len, ctx)
+        decode_launches()
         e2.record()
         enc_events.append((e0, e1))
         dec_events.append((e1, e2))
@@ -248,9 +285,8 @@ def main():
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            batch.encode_batch(src, coeffs, pieces, ctx)
-            if not args.encode_only:
-                batch.decode_batch_device(received, k, decoded, piece_status, object_status, data_len, ctx)
+            encode_launches()
+            decode_launches()
         run = g.replay
     elapsed = timed_loop(run, args.steps, args.warmup, dist, torch.cuda.synchronize)
     torch.cuda.synchronize()
@@ -345,6 +381,8 @@ def main():
             "k": k, "piece_bytes": L, "coded_per_object": n, "decoded_from": m, "objects_per_gpu": B,
             "parallelism": f"objects sharded over {dist.world} rank(s), no data-path collective",
             "kernel_variant": variant,
+            "pipeline": "elimination on a side stream concurrent with the encode data work" if args.pipeline
+                        else "serial",
         },
         "roofline": roofline,
         "hbm_single_pass_encode": single,

@@ -191,6 +191,13 @@ int rlnc_decoder_get_decoded_data_device(rlnc_decoder *dec, uint8_t *out_dev, si
 /* n coded pieces for each of num_objects objects (encoder.rs:241-250 × n × objects). */
 int rlnc_encode_batch(rlnc_context *ctx, const uint8_t *src_dev, size_t k, size_t L, size_t num_objects,
                       const uint8_t *coeffs_dev, size_t n, uint8_t *pieces_dev);
+/* rlnc_encode_batch in two parts, for pipelining a decoder's elimination against the data work (bench.py):
+ * the coefficient headers alone (pieces[o][i][0..k) = coeffs[o][i], one strided copy) and the data alone
+ * (pieces[o][i][k..k+L)).  Together they write exactly what rlnc_encode_batch writes. */
+int rlnc_encode_batch_headers(rlnc_context *ctx, const uint8_t *coeffs_dev, size_t k, size_t L, size_t num_objects,
+                              size_t n, uint8_t *pieces_dev);
+int rlnc_encode_batch_data(rlnc_context *ctx, const uint8_t *src_dev, size_t k, size_t L, size_t num_objects,
+                           const uint8_t *coeffs_dev, size_t n, uint8_t *pieces_dev);
 /* count recoded pieces per object from n received pieces: r [obj][count][n] → out [obj][count][k+L]
  * (recoder.rs:122-153; coefficient header and data are one linear combination of the full pieces). */
 int rlnc_recode_batch(rlnc_context *ctx, const uint8_t *pieces_dev, size_t k, size_t L, size_t n,
@@ -211,6 +218,17 @@ int rlnc_decode_batch(rlnc_context *ctx, const uint8_t *pieces_dev, size_t piece
 int rlnc_decode_batch_device(rlnc_context *ctx, const uint8_t *pieces_dev, size_t pieces_obj_stride, size_t k,
                              size_t L, size_t m, size_t num_objects, uint8_t *decoded_dev, int32_t *piece_status_dev,
                              int32_t *object_status_dev, int64_t *data_len_dev);
+
+/* rlnc_decode_batch_device in two parts (same results): the exact elimination, which reads only the k
+ * coefficient bytes of each piece — T_dev [obj][k][m] (decoded rows = T × received data rows; rows >= rank
+ * zero), per-piece statuses, ranks int32 [obj] — and the data side (T × data + the marker scan).  The two may
+ * run on different contexts/streams; the caller orders them (e.g. a HIP event). */
+int rlnc_decode_batch_eliminate(rlnc_context *ctx, const uint8_t *pieces_dev, size_t pieces_obj_stride, size_t k,
+                                size_t L, size_t m, size_t num_objects, uint8_t *T_dev, int32_t *piece_status_dev,
+                                int32_t *rank_dev);
+int rlnc_decode_batch_apply(rlnc_context *ctx, const uint8_t *pieces_dev, size_t pieces_obj_stride, size_t k,
+                            size_t L, size_t m, size_t num_objects, const uint8_t *T_dev, const int32_t *rank_dev,
+                            uint8_t *decoded_dev, int32_t *object_status_dev, int64_t *data_len_dev);
 
 /* ---- host-only: the decoder's exact coefficient elimination (no device needed) ---------------------------
  * The diagonal-pivot RREF of DecoderMatrix (decoder_matrix.rs:99-244) replicated on [coeffs | E] where E

@@ -80,6 +80,12 @@ _SIGS = {
     "rlnc_decoder_get_decoded_data": (C.c_int, [vp, vp, C.c_size_t, szp]),
     "rlnc_decoder_get_decoded_data_device": (C.c_int, [vp, vp, C.c_size_t, szp]),
     "rlnc_encode_batch": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, vp, C.c_size_t, vp]),
+    "rlnc_encode_batch_data": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, vp, C.c_size_t, vp]),
+    "rlnc_encode_batch_headers": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp]),
+    "rlnc_decode_batch_eliminate": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
+                                              vp, vp, vp]),
+    "rlnc_decode_batch_apply": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp,
+                                          vp, vp, vp, vp]),
     "rlnc_recode_batch": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp, C.c_size_t, vp]),
     "rlnc_decode_batch": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp, i32p,
                                     i32p, u64p]),

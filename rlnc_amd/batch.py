@@ -44,6 +44,29 @@ def encode_batch(src, coeffs, out, ctx: Context | None = None) -> None:
                                     C.c_void_p(out.data_ptr())), ctx.lib)
 
 
+def encode_batch_headers(coeffs, out, ctx: Context | None = None) -> None:
+    """The coefficient headers of encode_batch alone: out[o][i][0..k) = coeffs[o][i] (encoder.rs:246-248)."""
+    nobj, n, k = coeffs.shape
+    _chk(coeffs)
+    _chk(out)
+    assert out.shape[0] == nobj and out.shape[1] == n and out.shape[2] > k
+    ctx = _ctx_for(out, ctx)
+    check(ctx.lib.rlnc_encode_batch_headers(ctx.h, C.c_void_p(coeffs.data_ptr()), k, out.shape[2] - k, nobj, n,
+                                            C.c_void_p(out.data_ptr())), ctx.lib)
+
+
+def encode_batch_data(src, coeffs, out, ctx: Context | None = None) -> None:
+    """The data part of encode_batch alone: out[o][i][k..) = Σ_j coeffs[o][i][j]·src[o][j]."""
+    nobj, k, L = src.shape
+    n = coeffs.shape[1]
+    _chk(src)
+    _chk(coeffs, (nobj, n, k))
+    _chk(out, (nobj, n, k + L))
+    ctx = _ctx_for(src, ctx)
+    check(ctx.lib.rlnc_encode_batch_data(ctx.h, C.c_void_p(src.data_ptr()), k, L, nobj,
+                                         C.c_void_p(coeffs.data_ptr()), n, C.c_void_p(out.data_ptr())), ctx.lib)
+
+
 def recode_batch(pieces, r, out, k: int, ctx: Context | None = None) -> None:
     """out[o][c] = Σ_i r[o][c][i]·pieces[o][i] (coefficient header and data alike, recoder.rs:122-153)."""
     nobj, n, full = pieces.shape
@@ -97,6 +120,43 @@ def decode_batch_device(pieces, k: int, decoded, piece_status, object_status, da
                                            C.c_void_p(decoded.data_ptr()), C.c_void_p(piece_status.data_ptr()),
                                            C.c_void_p(object_status.data_ptr()), C.c_void_p(data_len.data_ptr())),
           ctx.lib)
+
+
+def _pieces_view(pieces, k):
+    nobj, m, full = pieces.shape
+    obj_stride = pieces.stride(0) if nobj > 1 else m * full
+    assert (m == 1 or pieces.stride(1) == full) and obj_stride >= m * full
+    return nobj, m, full - k, obj_stride
+
+
+def decode_batch_eliminate(pieces, k: int, T, piece_status, rank, ctx: Context | None = None):
+    """The elimination half of decode_batch_device (reads only the coefficient bytes): T uint8 [obj][k][m],
+    piece_status int32 [obj][m], rank int32 [obj] (device tensors), asynchronous on the current stream."""
+    import torch
+
+    nobj, m, L, obj_stride = _pieces_view(pieces, k)
+    _chk(T, (nobj, k, m))
+    assert piece_status.dtype == torch.int32 and tuple(piece_status.shape) == (nobj, m)
+    assert rank.dtype == torch.int32 and rank.numel() == nobj
+    ctx = _ctx_for(pieces, ctx)
+    check(ctx.lib.rlnc_decode_batch_eliminate(ctx.h, C.c_void_p(pieces.data_ptr()), obj_stride, k, L, m, nobj,
+                                              C.c_void_p(T.data_ptr()), C.c_void_p(piece_status.data_ptr()),
+                                              C.c_void_p(rank.data_ptr())), ctx.lib)
+
+
+def decode_batch_apply(pieces, k: int, T, rank, decoded, object_status, data_len, ctx: Context | None = None):
+    """The data half of decode_batch_device: decoded = T × received data, then the marker scan."""
+    import torch
+
+    nobj, m, L, obj_stride = _pieces_view(pieces, k)
+    _chk(T, (nobj, k, m))
+    _chk(decoded, (nobj, k, L))
+    assert object_status.dtype == torch.int32 and data_len.dtype == torch.int64
+    ctx = _ctx_for(pieces, ctx)
+    check(ctx.lib.rlnc_decode_batch_apply(ctx.h, C.c_void_p(pieces.data_ptr()), obj_stride, k, L, m, nobj,
+                                          C.c_void_p(T.data_ptr()), C.c_void_p(rank.data_ptr()),
+                                          C.c_void_p(decoded.data_ptr()), C.c_void_p(object_status.data_ptr()),
+                                          C.c_void_p(data_len.data_ptr())), ctx.lib)
 
 
 def matmul(coef, inp, out, ctx: Context | None = None) -> None:

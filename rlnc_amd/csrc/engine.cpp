@@ -751,8 +751,8 @@ int rlnc_decoder_get_decoded_data_device(rlnc_decoder *d, uint8_t *out_dev, size
 // ------------------------------------------------------------------------------------------------------
 // batch API
 // ------------------------------------------------------------------------------------------------------
-int rlnc_encode_batch(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t nobj, const uint8_t *coeffs,
-                      size_t n, uint8_t *pieces) {
+static int encode_batch_impl(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t nobj,
+                             const uint8_t *coeffs, size_t n, uint8_t *pieces, bool headers) {
     CHECK_ARG(ctx != nullptr);
     if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
     if (L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;
@@ -771,7 +771,7 @@ int rlnc_encode_batch(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L,
     p.out = pieces + k;
     p.out_obj = int64_t(n) * full;
     p.out_row = full;
-    p.hdr = pieces;
+    p.hdr = headers ? pieces : nullptr;
     p.hdr_obj = int64_t(n) * full;
     p.hdr_row = full;
     p.n_out = int(n);
@@ -779,6 +779,30 @@ int rlnc_encode_batch(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L,
     p.width = int64_t(L);
     p.n_obj = int(nobj);
     return ctx->matmul(p);
+}
+
+int rlnc_encode_batch(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t nobj, const uint8_t *coeffs,
+                      size_t n, uint8_t *pieces) {
+    return encode_batch_impl(ctx, src, k, L, nobj, coeffs, n, pieces, true);
+}
+
+int rlnc_encode_batch_data(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t nobj,
+                           const uint8_t *coeffs, size_t n, uint8_t *pieces) {
+    return encode_batch_impl(ctx, src, k, L, nobj, coeffs, n, pieces, false);
+}
+
+int rlnc_encode_batch_headers(rlnc_context *ctx, const uint8_t *coeffs, size_t k, size_t L, size_t nobj, size_t n,
+                              uint8_t *pieces) {
+    CHECK_ARG(ctx != nullptr);
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
+    if (L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;
+    if (n == 0 || nobj == 0) return RLNC_OK;
+    CHECK_ARG(coeffs && pieces);
+    int st = ctx->activate();
+    if (st) return st;
+    // pieces[o][i][0..k) = coeffs[o][i] (encoder.rs:246-248): one strided copy
+    HIP_TRY(hipMemcpy2DAsync(pieces, k + L, coeffs, k, k, n * nobj, hipMemcpyDeviceToDevice, ctx->stream));
+    return RLNC_OK;
 }
 
 int rlnc_recode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t k, size_t L, size_t n, size_t nobj,
@@ -811,12 +835,11 @@ int rlnc_recode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t k, size_t
 
 // Device path: exact elimination on the device (rref.hip) → T × data (one matmul) → marker scan.
 // Everything is enqueued on the context stream; outputs stay on the device.
-static int decode_batch_device_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
-                                    size_t m, size_t nobj, uint8_t *decoded, int32_t *pstat_dev, int32_t *ostat_dev,
-                                    int64_t *len_dev, int32_t *rank_dev) {
+// The elimination alone: reads only the k coefficient bytes of each piece; writes T [obj][k][m], the per-piece
+// statuses and the ranks.
+static int decode_eliminate_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
+                                 size_t m, size_t nobj, uint8_t *T, int32_t *pstat_dev, int32_t *rank_dev) {
     const size_t full = k + L;
-    int st;
-    if ((st = ctx->ws_coef.ensure(nobj * k * m)) || (st = ctx->ws_scan.ensure(nobj * 8))) return st;
     rlnc::RrefParams rp{};
     rp.pieces = pieces;
     rp.obj_stride = int64_t(obj_stride);
@@ -824,17 +847,27 @@ static int decode_batch_device_impl(rlnc_context *ctx, const uint8_t *pieces, si
     rp.k = int(k);
     rp.m = int(m);
     rp.n_obj = int(nobj);
-    rp.T = ctx->ws_coef.as<uint8_t>();
+    rp.T = T;
     rp.T_obj = int64_t(k * m);
     rp.status = pstat_dev;
     rp.rank = rank_dev;
     rp.lds_only = ctx->decode_path == 3 ? 1 : ctx->decode_path == 4 ? 2 : 0;
     HIP_TRY(rlnc::launch_rref_batch(rp, ctx->stream));
+    return RLNC_OK;
+}
+
+// The data side: decoded = T × received data (one matmul), then the marker scan (decoder.rs:136-177).
+static int decode_apply_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
+                             size_t m, size_t nobj, const uint8_t *T, const int32_t *rank_dev, uint8_t *decoded,
+                             int32_t *ostat_dev, int64_t *len_dev) {
+    const size_t full = k + L;
+    int st;
+    if ((st = ctx->ws_scan.ensure(nobj * 8))) return st;
     rlnc::MatmulParams p{};
     p.in = pieces + k;
     p.in_obj = int64_t(obj_stride);
     p.in_row = int64_t(full);
-    p.coef = ctx->ws_coef.as<uint8_t>();
+    p.coef = T;
     p.coef_obj = int64_t(k * m);
     p.coef_row = int64_t(m);
     p.out = decoded;
@@ -848,6 +881,16 @@ static int decode_batch_device_impl(rlnc_context *ctx, const uint8_t *pieces, si
     HIP_TRY(rlnc::launch_final_data_len_ranked(decoded, int64_t(k * L), int64_t(k * L), int(nobj), int(k), rank_dev,
                                                ctx->ws_scan.as<unsigned long long>(), ostat_dev, len_dev, ctx->stream));
     return RLNC_OK;
+}
+
+static int decode_batch_device_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
+                                    size_t m, size_t nobj, uint8_t *decoded, int32_t *pstat_dev, int32_t *ostat_dev,
+                                    int64_t *len_dev, int32_t *rank_dev) {
+    int st;
+    if ((st = ctx->ws_coef.ensure(nobj * k * m))) return st;
+    uint8_t *T = ctx->ws_coef.as<uint8_t>();
+    if ((st = decode_eliminate_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, pstat_dev, rank_dev))) return st;
+    return decode_apply_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, rank_dev, decoded, ostat_dev, len_dev);
 }
 
 // Host path (matrices too large for LDS): exact elimination on host threads (elimination.hpp).
@@ -909,7 +952,7 @@ static int decode_batch_host_impl(rlnc_context *ctx, const uint8_t *pieces, size
     p.in = pieces + k;
     p.in_obj = int64_t(obj_stride);
     p.in_row = int64_t(full);
-    p.coef = ctx->ws_coef.as<uint8_t>();
+    p.coef = T;
     p.coef_obj = int64_t(k * m);
     p.coef_row = int64_t(m);
     p.out = decoded;
@@ -994,6 +1037,30 @@ int rlnc_decode_batch_device(rlnc_context *ctx, const uint8_t *pieces, size_t ob
     if ((st = ctx->ws_rank.ensure(nobj * 4))) return st;
     return decode_batch_device_impl(ctx, pieces, obj_stride, k, L, m, nobj, decoded, piece_status_dev,
                                     object_status_dev, data_len_dev, ctx->ws_rank.as<int32_t>());
+}
+
+int rlnc_decode_batch_eliminate(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
+                                size_t m, size_t nobj, uint8_t *T_dev, int32_t *piece_status_dev, int32_t *rank_dev) {
+    if (nobj == 0 && ctx) return RLNC_OK;
+    CHECK_ARG(T_dev != nullptr);
+    int st = decode_batch_check(ctx, pieces, obj_stride, k, L, m, nobj, T_dev);
+    if (st) return st;
+    CHECK_ARG(piece_status_dev && rank_dev);
+    if (rlnc::rref_lds_bytes(int(k), int(m)) > rlnc::kRrefMaxLds)
+        return set_error(RLNC_ERR_INVALID_ARGUMENT, "k=%zu, m=%zu exceed the device elimination's LDS budget; use "
+                         "rlnc_decode_batch", k, m);
+    return decode_eliminate_impl(ctx, pieces, obj_stride, k, L, m, nobj, T_dev, piece_status_dev, rank_dev);
+}
+
+int rlnc_decode_batch_apply(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L, size_t m,
+                            size_t nobj, const uint8_t *T_dev, const int32_t *rank_dev, uint8_t *decoded,
+                            int32_t *object_status_dev, int64_t *data_len_dev) {
+    if (nobj == 0 && ctx) return RLNC_OK;
+    int st = decode_batch_check(ctx, pieces, obj_stride, k, L, m, nobj, decoded);
+    if (st) return st;
+    CHECK_ARG(T_dev && rank_dev && object_status_dev && data_len_dev);
+    return decode_apply_impl(ctx, pieces, obj_stride, k, L, m, nobj, T_dev, rank_dev, decoded, object_status_dev,
+                             data_len_dev);
 }
 
 // ------------------------------------------------------------------------------------------------------

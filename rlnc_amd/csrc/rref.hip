@@ -552,7 +552,7 @@ __device__ int reg_run(const Mat &M, const uint32_t *tab, uint32_t (&v)[RT], con
 // ---------------------------------------------------------------------------------------------------
 template <int NW, int MG, int RTW>
 __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, uint32_t *P, int m, int k, int &rows,
-                          bool &clean, int32_t *St) {
+                          bool &clean, int32_t *St PROF_ARGS) {
     constexpr int G = MG, DP = 64 / MG;
     constexpr bool kPre = RTW <= 8;  // few rows per lane: the next piece's forward tables are prefetched
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -612,7 +612,9 @@ __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, u
         for (int sh = DP; sh < 64; sh <<= 1) acc ^= __shfl_xor(acc, sh);
         uint32_t *Pb = P + buf * NW * DP;
         if (lane < DP) Pb[wave * DP + lane] = acc;
+        PROF_MARK(2);
         __syncthreads();
+        PROF_MARK(3);
         uint32_t nr = init;
 #pragma unroll
         for (int s = 0; s < NW; ++s) nr ^= Pb[s * DP + w];
@@ -639,6 +641,7 @@ __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, u
         nr = (nr & ~mask) | (mul4t(ti4, ti2, nr) & mask);
         if (w == rw) nr = (nr & ~(0xFFu << rb)) | (1u << rb);
         rows = r + 1;
+        PROF_MARK(4);
 #pragma unroll
         for (int c0 = 0; c0 < RTW; c0 += 8) {  // backward in chunks of 8 rows (table reads issued together)
             constexpr int U = RTW < 8 ? RTW : 8;
@@ -658,6 +661,7 @@ __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, u
         for (int t = 0; t < RTW; ++t)
             if (row_of(t) == r) v[t] = nr;
         if (threadIdx.x == 0) St[pc] = RLNC_OK;
+        PROF_MARK(5);
     }
     to_lds(rows);
     __syncthreads();
@@ -677,6 +681,7 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, in
     const int k = p.k, m = p.m;
 #ifdef RLNC_RREF_PROFILE  // diagnostic build: statuses become per-piece cycle counts, rank the setup cycles
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();  // 100 MHz
 #endif
     Mat M;
     M.D = rref_row_dwords(k, m);
@@ -726,9 +731,10 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, in
     uint64_t prof_t = t_setup;
 #endif
     if constexpr (NW > 1) {
-        pc0 = reg_run_mw<NW, MG, MRTW>(M, tab, H, P, m, k, rows, clean, St);
+        pc0 = reg_run_mw<NW, MG, MRTW>(M, tab, H, P, m, k, rows, clean, St PROF_PASS);
         if (threadIdx.x >= 64) return;  // wave 0 finishes alone (generic path / output)
-#ifdef RLNC_RREF_PROFILE  // diagnostic: slot 0 = setup cycles, slot 1 = the multi-wave clean run
+#ifdef RLNC_RREF_PROFILE  // diagnostic: slot 0 = setup cycles, slot 1 = the multi-wave clean run; 2-5 its
+        // phases (2 forward + partial-sum write, 3 barrier, 4 partial-sum read + normalise, 5 backward)
         prof[0] = t_setup - t_start;
         prof[1] = __builtin_amdgcn_s_memtime() - t_setup;
         prof_t = __builtin_amdgcn_s_memtime();
@@ -782,6 +788,10 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, in
         if (clean && pc0 < m) regs_to_lds<G, RT>(M, v, rows);
     __syncthreads();
 #ifdef RLNC_RREF_PROFILE  // phases: 0 row init, 1 spare copy, 2 forward, 3 normalise, 4 backward, 5 generic, 6 is_clean, 7 status
+    if constexpr (NW > 1) {  // multi-wave: 6 = shader cycles from kernel entry to here, 7 = the same in 10 ns
+        prof[6] = __builtin_amdgcn_s_memtime() - t_start;
+        prof[7] = __builtin_amdgcn_s_memrealtime() - rt_start;
+    }
     if (lane == 0)
         for (int i = 0; i < 8 && i < m; ++i) St[i] = int32_t(prof[i]);
     __syncthreads();
@@ -797,6 +807,11 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, in
         const int r = e / m, s = e % m;
         T[e] = r < rows ? M.b[r * M.S + k + s] : uint8_t(0);
     }
+#ifdef RLNC_RREF_PROFILE  // status 5 of each object = 10 ns ticks from entry to every output store completed
+    __builtin_amdgcn_s_waitcnt(0);
+    if (lane == 0 && m > 5) p.status[int64_t(o) * m + 5] = int32_t(__builtin_amdgcn_s_memrealtime() - rt_start);
+    if (lane == 0 && m > 4) p.status[int64_t(o) * m + 4] = int32_t(rt_start & 0x7FFFFFFFu);  // entry tick
+#endif
 }
 
 }  // namespace

@@ -361,6 +361,64 @@ def test_decode_batch_device_async_outputs(ctx, orc):
             assert np.array_equal(decoded[o].cpu().numpy().reshape(-1)[: data[o].size], data[o])
 
 
+@pytest.mark.parametrize("k,L,n,m,dep", [(32, 4096 * 3 + 16, 40, 32, 0.0), (16, 5000, 24, 20, 0.3), (64, 8192, 64, 64, 0.0)])
+def test_split_encode_decode_pipeline(ctx, orc, k, L, n, m, dep):
+    """encode_batch_headers + encode_batch_data == encode_batch, and decode_batch_eliminate on a second context /
+    stream (ordered by HIP events) + decode_batch_apply == decode_batch_device, byte for byte (bench.py's
+    pipelined step)."""
+    import torch
+
+    import rlnc_amd
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(k * 7 + m)
+    nobj = 5
+    src = dev(rng.integers(0, 256, (nobj, k, L), dtype=np.uint8))
+    co = rng.integers(0, 256, (nobj, n, k), dtype=np.uint8)
+    for o in range(nobj):  # some dependent coding vectors: useless pieces and rank < k objects
+        for p in range(2, m):
+            if rng.random() < dep:
+                co[o, p] = co[o, p - 1] ^ co[o, p - 2]
+    co = dev(co)
+    ref = torch.empty((nobj, n, k + L), dtype=torch.uint8, device="cuda:0")
+    batch.encode_batch(src, co, ref, ctx)
+    pieces = torch.zeros_like(ref)
+    ctx2 = rlnc_amd.Context(0)
+    side = torch.cuda.Stream()
+    ev_h, ev_e = torch.cuda.Event(), torch.cuda.Event()
+    T = torch.empty((nobj, k, m), dtype=torch.uint8, device="cuda:0")
+    pst = torch.full((nobj, m), -1, dtype=torch.int32, device="cuda:0")
+    rank = torch.empty(nobj, dtype=torch.int32, device="cuda:0")
+    dec = torch.zeros((nobj, k, L), dtype=torch.uint8, device="cuda:0")
+    ost = torch.empty(nobj, dtype=torch.int32, device="cuda:0")
+    dl = torch.empty(nobj, dtype=torch.int64, device="cuda:0")
+    batch.encode_batch_headers(co, pieces, ctx)
+    ev_h.record()
+    batch.encode_batch_data(src, co, pieces, ctx)
+    with torch.cuda.stream(side):
+        side.wait_event(ev_h)
+        batch.decode_batch_eliminate(pieces[:, :m], k, T, pst, rank, ctx2)
+        ev_e.record()
+    torch.cuda.current_stream().wait_event(ev_e)
+    batch.decode_batch_apply(pieces[:, :m], k, T, rank, dec, ost, dl, ctx)
+    torch.cuda.synchronize()
+    assert torch.equal(pieces, ref)
+    want_dec = torch.zeros_like(dec)
+    want_ps = torch.empty_like(pst)
+    want_os = torch.empty_like(ost)
+    want_dl = torch.empty_like(dl)
+    batch.decode_batch_device(ref[:, :m], k, want_dec, want_ps, want_os, want_dl, ctx)
+    torch.cuda.synchronize()
+    assert torch.equal(pst, want_ps) and torch.equal(ost, want_os) and torch.equal(dec, want_dec)
+    assert torch.equal(dl[ost == 0], want_dl[want_os == 0])
+    assert torch.equal(rank, (pst == 0).sum(1).to(torch.int32))
+    hs = host(src)
+    for o in range(nobj):
+        if int(rank[o]) == k:
+            assert np.array_equal(host(dec)[o], hs[o]), o
+    ctx2.close()
+
+
 # ------------------------------------------------------------------------------------------------
 # ports of src/full/tests.rs (round trips with random sizes, recoders, useless pieces)
 # ------------------------------------------------------------------------------------------------
