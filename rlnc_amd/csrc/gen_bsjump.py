@@ -30,7 +30,10 @@ A call is 4 scalar instructions (M0, low address half, s_swappc_b64, the block's
 is preset once the prologue has checked that the block table does not straddle a 4 GiB line (else the loop
 copy with the carry runs), and rows past n_out have c = 0, whose block returns at once.
 
-Shared-combination program (RLNC_BSJ_ASM_W4S, variant 7): with 4 waves on one column block, wave w builds
+Shared-combination program (RLNC_BSJ_ASM_W4S, variant 7) calls absolute block addresses: the offset kernel writes
+base + c * BLOCK_BYTES (64-bit; the base is read once per device by a probe launch of this program, which stores
+it and exits), two s_load_dwordx16 buffers of 8 addresses, so a call is s_mov m0 + s_swappc_b64 + s_setpc_b64.
+With 4 waves on one column block, wave w builds
 only set w = (group w >> 1, half w & 1) of the plane combinations -- half of one group's transpose + 11 XORs
 instead of two full transposes + 44 XORs -- and the four sets (4 KiB each) are exchanged through two 16 KiB
 LDS slots.  Per source row j: barrier; 16 ds_read_b128 of row j's sets; the staging read of row j + 2 (the
@@ -84,7 +87,12 @@ def OWN(x):  # the wave's own set of the next row, built here and written to LDS
 
 S_NDMA, S_H = 78, 79  # source rows still to advance over; the wave's half h
 CS_SLOT, CS_SET = 16384, 4096
-LAST_VGPR_ALL, LAST_SGPR_ALL = 243, S_H
+# the shared program reads absolute 64-bit block addresses (the offset kernel adds the table base found by a probe
+# launch): two buffers of 8 address pairs (s_load_dwordx16), the other scalars moved up
+S_ADDR = (36, 52)
+SHARED_SGPRS = dict(S_SRC=68, S_IDX=70, S_DST=72, S_BASE=74, S_TGT=76, S_RET=78, S_INROW=80, S_OUTROW=81, S_CNT=82,
+                    S_ROWS=83, S_T0=84, S_LDSW=85, S_NDMA=86, S_H=87)
+LAST_VGPR_ALL, LAST_SGPR_ALL = 243, 87
 
 DIAG = set()
 ALIGN = 0  # log2 alignment of the first block (--align)
@@ -353,11 +361,11 @@ def body_s(L, j):
               for q in range(4)]
     else:
         own_set(L, (j + 1) % 2, (j + 1) % 2)
-    cur, nxt = S_OFF[j % 3], S_OFF[(j + 1) % 3]
+    cur, nxt = S_ADDR[j % 2], S_ADDR[(j + 1) % 2]
     L += [
         # the 16 set reads (LDS returns in order; 2 staging reads + 4 writes may fly)
         "s_waitcnt lgkmcnt(6)" if "snowait" not in DIAG else "s_nop 0",
-        f"s_load_dwordx8 s[{nxt}:{nxt + 7}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
+        f"s_load_dwordx16 s[{nxt}:{nxt + 15}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
         f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
         f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
         "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)",
@@ -369,12 +377,24 @@ def body_s(L, j):
             L += [f"v_bitop3_b32 v{ACC(0, g, o)}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])}, v{ACC(0, g, o)} bitop3:0x96"
                   for g in range(2) for o in range(8)]
             continue
-        call(L, cur, i)
+        # row i: M0 = its accumulator slot, then the call to the absolute address of block c (rows past
+        # n_out have c = 0, whose block returns at once)
+        L += [f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}",
+              f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{cur + 2 * i}:{cur + 2 * i + 1}]"]
     L.append("s_set_gpr_idx_off")
 
 
 def program_shared():
     assert WAVES == 4
+    saved = {n: globals()[n] for n in SHARED_SGPRS}
+    globals().update(SHARED_SGPRS)
+    try:
+        return program_shared_body()
+    finally:
+        globals().update(saved)
+
+
+def program_shared_body():
     L = [
         f"s_mov_b64 s[{S_SRC}:{S_SRC + 1}], %[src]",
         f"s_mov_b64 s[{S_IDX}:{S_IDX + 1}], %[idx]",
@@ -393,13 +413,23 @@ def program_shared():
         f"s_add_u32 s{S_BASE}, s{S_BASE}, (9f - 5b)",
         f"s_addc_u32 s{S_BASE + 1}, s{S_BASE + 1}, 0",
         f"s_mov_b32 s{S_LDSW}, %[ldsw]",
+        # probe launch (probe != 0): store the block table's address for the offset kernel and leave
+        "s_cmp_lg_u64 %[probe], 0",
+        "s_cbranch_scc0 10f",
+        f"v_mov_b32 v{V_X}, s{S_BASE}",
+        f"v_mov_b32 v{V_X + 1}, s{S_BASE + 1}",
+        f"v_mov_b32 v{V_X + 2}, 0",
+        f"global_store_dwordx2 v{V_X + 2}, v[{V_X}:{V_X + 1}], %[probe]",
+        "s_waitcnt vmcnt(0)",
+        "s_branch 8f",
+        "10:",
     ]
     dmai = "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)
     for slot in range(3):  # rows 0, 1, 2 (clamped to the last row) into ring slots 0, 1, 2
         if slot:
             advance_s(L)
         L += [f"s_add_u32 m0, s{S_LDSW}, {slot * 4096}", "s_nop 0", dmai]
-    L.append(f"s_load_dwordx8 s[{S_OFF[0]}:{S_OFF[0] + 7}], s[{S_IDX}:{S_IDX + 1}], 0")
+    L.append(f"s_load_dwordx16 s[{S_ADDR[0]}:{S_ADDR[0] + 15}], s[{S_IDX}:{S_IDX + 1}], 0")
     L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
     L.append(f"v_mov_b32 v{OWN(0)}, 0")
     L += ["s_waitcnt vmcnt(1)", "s_barrier"]  # rows 0 and 1 landed (all waves)
@@ -411,7 +441,11 @@ def program_shared():
     advance_s(L)
     L += [f"s_add_u32 m0, s{S_LDSW}, 0", "s_nop 0", dmai]
     own_set(L, 0, 0)  # row 0's own set into set slot 0
-    loops(L, body_s, 6)
+    L.append("1:")  # absolute addresses: one loop (no carry case)
+    for j in range(6):
+        body_s(L, j)
+        L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f" if j < 5 else "s_cbranch_scc0 1b"]
+    L += ["3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
     epilogue(L)
     L.append("s_branch 8f")
     L.append("9:")
@@ -501,7 +535,7 @@ def main():
             body_txt = "\\n\\t".join(program())
             f.write(f'#define RLNC_BSJ_ASM_W{w} "{body_txt}"\n')
         WAVES, WG_ROWS = 4, NT * 4
-        STREAM_J_BYTES = WG_ROWS * 4
+        STREAM_J_BYTES = WG_ROWS * 8  # 64-bit block addresses
         body_txt = "\\n\\t".join(program_shared())
         f.write(f'#define RLNC_BSJ_ASM_W4S "{body_txt}"\n')
         f.write(f"#define RLNC_BSJ_CSET_BYTES {2 * CS_SLOT}\n")

@@ -19,6 +19,8 @@
 // north-star's literal design; it is kept as the ablation baseline.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include "../../include/rlnc_hip.h"
 #include "gf256.hpp"
 #include "kernels.hpp"
@@ -773,10 +775,12 @@ hipError_t launch_bs(const MatmulParams &p, hipStream_t s, void *scratch, size_t
 constexpr int kBsjWaveRows = RLNC_BSJ_NT;  // output rows per wave; a workgroup of W waves = 8 W rows
 constexpr int kBsjColBlock = 4096;          // 64 lanes × 64 B, shared by the W waves
 
-// stream[obj][row tile][j][row in tile] = c · RLNC_BSJ_BLOCK_BYTES (c = 0 for rows past n_out)
+// stream[obj][row tile][j][row in tile] = c · RLNC_BSJ_BLOCK_BYTES (c = 0 for rows past n_out); ABS: the
+// block's absolute address base + c · RLNC_BSJ_BLOCK_BYTES (64-bit, the shared-set program calls it directly)
+template <bool ABS>
 __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, int64_t coef_obj, int64_t coef_row,
                                                          int n_out, int n_in, int row_tiles, int tile_rows,
-                                                         uint32_t *stream) {
+                                                         void *stream, uint64_t base) {
     const int64_t per_obj = int64_t(row_tiles) * n_in * tile_rows;
     const int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     const int obj = blockIdx.y;
@@ -786,14 +790,18 @@ __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, in
     const int rt = int(e / (int64_t(tile_rows) * n_in));
     const int row = rt * tile_rows + i;
     const uint32_t c = row < n_out ? coef[int64_t(obj) * coef_obj + int64_t(row) * coef_row + j] : 0u;
-    stream[int64_t(obj) * per_obj + e] = c * uint32_t(RLNC_BSJ_BLOCK_BYTES);
+    if constexpr (ABS)
+        static_cast<uint64_t *>(stream)[int64_t(obj) * per_obj + e] = base + uint64_t(c) * RLNC_BSJ_BLOCK_BYTES;
+    else
+        static_cast<uint32_t *>(stream)[int64_t(obj) * per_obj + e] = c * uint32_t(RLNC_BSJ_BLOCK_BYTES);
 }
 
 // SHARE (W = 4 only): wave w builds one of the four combination sets of each source row and the sets are
 // exchanged through LDS (RLNC_BSJ_ASM_W4S) instead of every wave building all four
+// probe != nullptr (SHARE only): store the block table's address there and return (launch_bsj, once per device)
 template <int W, bool SHARE = false>
-__global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const uint32_t *stream, int row_tiles,
-                                                               int col_blocks) {
+__global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const void *stream, int row_tiles,
+                                                               int col_blocks, uint64_t *probe) {
     static_assert(!SHARE || W == 4, "the shared-set program is generated for 4 waves");
     constexpr int kTileRows = kBsjWaveRows * W;
     __shared__ __attribute__((aligned(16))) uint8_t ring[RLNC_BSJ_SLOTS * kBsjColBlock];
@@ -816,7 +824,9 @@ __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, c
     const uint8_t *src = p.in + int64_t(obj) * p.in_obj + int64_t(cb) * kBsjColBlock;
     uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0 + kBsjWaveRows * w) * p.out_row +
                    int64_t(cb) * kBsjColBlock;
-    const uint32_t *idx = stream + (int64_t(obj) * row_tiles + rt) * p.n_in * kTileRows + kBsjWaveRows * w;
+    constexpr int kEntry = SHARE ? 8 : 4;  // bytes per stream entry: absolute address / block offset
+    const uint8_t *idx = static_cast<const uint8_t *>(stream) +
+                         ((int64_t(obj) * row_tiles + rt) * p.n_in * kTileRows + kBsjWaveRows * w) * kEntry;
     typedef __attribute__((address_space(3))) uint8_t lds_u8;
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)ring));  // addrspacecast
     constexpr uint32_t kShare = kBsjColBlock / W;  // bytes of each row a wave moves into the ring
@@ -834,7 +844,7 @@ __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, c
     : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),                           \
       [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw), [off] "v"(off), \
       [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr), [ldsc] "v"(ldsc), [ldscw] "v"(ldscw), [ldsrg] "v"(ldsrg),           \
-      [half] "s"(half)                                                                                            \
+      [half] "s"(half), [probe] "s"(probe)                                                                        \
     : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S
     if constexpr (W == 1) asm volatile(RLNC_BSJ_ASM_W1 : RLNC_BSJ_OPERANDS);
     if constexpr (W == 2) asm volatile(RLNC_BSJ_ASM_W2 : RLNC_BSJ_OPERANDS);
@@ -856,8 +866,37 @@ bool bsj_eligible(const MatmulParams &p, bool aligned) {
 size_t bsj_scratch_bytes(const MatmulParams &p) {
     const int tile_rows = kBsjWaveRows * bsj_waves(p.n_out);
     const int64_t tiles = (p.n_out + tile_rows - 1) / tile_rows;
-    // + one source: the main loop loads the offsets of the source after the last one
-    return size_t(int64_t(p.n_obj) * tiles * p.n_in * tile_rows * 4 + 256);
+    // 8 bytes per entry (absolute addresses of the shared program, 4 otherwise) + one source: the main loop
+    // loads the entries of the source after the last one
+    return size_t(int64_t(p.n_obj) * tiles * p.n_in * tile_rows * 8 + 512);
+}
+
+// Address of the shared-set program's block table on the current device: one probe launch per device (the
+// code object does not move while the process runs).  Synchronous on `s` the first time only.
+static hipError_t bsj_shared_base(hipStream_t s, void *scratch, uint64_t &base) {
+    static std::mutex mu;
+    static uint64_t bases[64] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lock(mu);
+    if (bases[dev] == 0) {
+        MatmulParams q{};
+        q.n_obj = 1;
+        q.n_out = 1;
+        q.n_in = 1;
+        uint64_t *slot = static_cast<uint64_t *>(scratch);
+        hipLaunchKernelGGL((gf_matmul_bsj_kernel<4, true>), dim3(1), dim3(256), 0, s, q, scratch, 1, 1, slot);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        uint64_t h = 0;
+        if ((e = hipMemcpyAsync(&h, slot, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (h == 0) return hipErrorLaunchFailure;
+        bases[dev] = h;
+    }
+    base = bases[dev];
+    return hipSuccess;
 }
 
 hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full,
@@ -869,27 +908,38 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
     const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
     if (scratch == nullptr || scratch_bytes < bsj_scratch_bytes(p)) return hipErrorInvalidValue;
     if (total > 0x7FFFFFFFLL || p.n_obj > 65535) return hipErrorInvalidValue;
-    uint32_t *stream = static_cast<uint32_t *>(scratch);
+    const bool abs = share && W == 4;  // the shared-set program calls absolute block addresses
+    uint64_t base = 0;
+    if (abs) {
+        hipError_t e = bsj_shared_base(s, scratch, base);
+        if (e != hipSuccess) return e;
+    }
+    void *stream = scratch;
     const int64_t per_obj = int64_t(row_tiles) * p.n_in * tile_rows;
     if ((per_obj + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(bsj_offset_kernel, dim3(unsigned((per_obj + 255) / 256), unsigned(p.n_obj)), dim3(256), 0, s,
-                       p.coef, p.coef_obj, p.coef_row, p.n_out, p.n_in, row_tiles, tile_rows, stream);
+    const dim3 og(unsigned((per_obj + 255) / 256), unsigned(p.n_obj));
+    if (abs)
+        hipLaunchKernelGGL(bsj_offset_kernel<true>, og, dim3(256), 0, s, p.coef, p.coef_obj, p.coef_row, p.n_out,
+                           p.n_in, row_tiles, tile_rows, stream, base);
+    else
+        hipLaunchKernelGGL(bsj_offset_kernel<false>, og, dim3(256), 0, s, p.coef, p.coef_obj, p.coef_row, p.n_out,
+                           p.n_in, row_tiles, tile_rows, stream, uint64_t(0));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     MatmulParams q = p;
     q.width = full;
     if (W == 1)
         hipLaunchKernelGGL(gf_matmul_bsj_kernel<1>, dim3(unsigned(total)), dim3(64), 0, s, q, stream, row_tiles,
-                           col_blocks);
+                           col_blocks, nullptr);
     else if (W == 2)
         hipLaunchKernelGGL(gf_matmul_bsj_kernel<2>, dim3(unsigned(total)), dim3(128), 0, s, q, stream, row_tiles,
-                           col_blocks);
+                           col_blocks, nullptr);
     else if (share)
         hipLaunchKernelGGL((gf_matmul_bsj_kernel<4, true>), dim3(unsigned(total)), dim3(256), 0, s, q, stream,
-                           row_tiles, col_blocks);
+                           row_tiles, col_blocks, nullptr);
     else
         hipLaunchKernelGGL(gf_matmul_bsj_kernel<4>, dim3(unsigned(total)), dim3(256), 0, s, q, stream, row_tiles,
-                           col_blocks);
+                           col_blocks, nullptr);
     return hipGetLastError();
 }
 
