@@ -800,8 +800,10 @@ int rlnc_encode_batch_headers(rlnc_context *ctx, const uint8_t *coeffs, size_t k
     CHECK_ARG(coeffs && pieces);
     int st = ctx->activate();
     if (st) return st;
-    // pieces[o][i][0..k) = coeffs[o][i] (encoder.rs:246-248): one strided copy
-    HIP_TRY(hipMemcpy2DAsync(pieces, k + L, coeffs, k, k, n * nobj, hipMemcpyDeviceToDevice, ctx->stream));
+    // pieces[o][i][0..k) = coeffs[o][i] (encoder.rs:246-248): one strided copy (a kernel: the runtime's 2D
+    // blit took 36 µs for 1,024 rows of 32 B)
+    HIP_TRY(rlnc::launch_copy_rows(pieces, int64_t(k + L), coeffs, int64_t(k), int64_t(k), int64_t(n * nobj),
+                                   ctx->stream));
     return RLNC_OK;
 }
 

@@ -943,6 +943,25 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
     return hipGetLastError();
 }
 
+// strided row copy (the coded pieces' coefficient headers, encoder.rs:246-248): one byte per thread
+__global__ __launch_bounds__(256) void copy_rows_kernel(uint8_t *dst, int64_t dst_stride, const uint8_t *src,
+                                                        int64_t src_stride, int64_t width, int64_t total) {
+    const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (e >= total) return;
+    const int64_t r = e / width, c = e % width;
+    dst[r * dst_stride + c] = src[r * src_stride + c];
+}
+
+hipError_t launch_copy_rows(uint8_t *dst, int64_t dst_stride, const uint8_t *src, int64_t src_stride, int64_t width,
+                            int64_t rows, hipStream_t s) {
+    const int64_t total = width * rows;
+    if (total <= 0) return hipSuccess;
+    if ((total + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(copy_rows_kernel, dim3(unsigned((total + 255) / 256)), dim3(256), 0, s, dst, dst_stride, src,
+                       src_stride, width, total);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------------------
 // element-wise primitives (simd/mod.rs:18-119); the scalar early-outs are taken on the host
 // ---------------------------------------------------------------------------------------------------

@@ -49,6 +49,9 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t stream, MatmulVarian
 // Element-wise primitives (src/common/simd/mod.rs:18-119) on one device vector.
 hipError_t launch_mul_vec_by_scalar(uint8_t *vec, int64_t len, uint8_t scalar, hipStream_t s);
 hipError_t launch_add_vectors(uint8_t *dst, const uint8_t *src, int64_t len, hipStream_t s);
+// dst[r][0..width) = src[r][0..width) for rows r < rows (strided byte rows, e.g. coded-piece headers)
+hipError_t launch_copy_rows(uint8_t *dst, int64_t dst_stride, const uint8_t *src, int64_t src_stride, int64_t width,
+                            int64_t rows, hipStream_t s);
 hipError_t launch_mul_add(uint8_t *dst, const uint8_t *src, int64_t len, uint8_t scalar, hipStream_t s);
 
 // decoder.rs:162-177 on device, per object: finds the last nonzero byte of the padded payload
