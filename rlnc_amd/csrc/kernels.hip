@@ -952,16 +952,6 @@ __global__ __launch_bounds__(256) void copy_rows_kernel(uint8_t *dst, int64_t ds
     dst[r * dst_stride + c] = src[r * src_stride + c];
 }
 
-hipError_t launch_copy_rows(uint8_t *dst, int64_t dst_stride, const uint8_t *src, int64_t src_stride, int64_t width,
-                            int64_t rows, hipStream_t s) {
-    const int64_t total = width * rows;
-    if (total <= 0) return hipSuccess;
-    if ((total + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(copy_rows_kernel, dim3(unsigned((total + 255) / 256)), dim3(256), 0, s, dst, dst_stride, src,
-                       src_stride, width, total);
-    return hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------------------------------
 // element-wise primitives (simd/mod.rs:18-119); the scalar early-outs are taken on the host
 // ---------------------------------------------------------------------------------------------------
@@ -1074,6 +1064,16 @@ __global__ void final_len_ranked_kernel(const uint8_t *data, int64_t obj_stride,
 }
 
 }  // namespace
+
+hipError_t launch_copy_rows(uint8_t *dst, int64_t dst_stride, const uint8_t *src, int64_t src_stride, int64_t width,
+                            int64_t rows, hipStream_t s) {
+    const int64_t total = width * rows;
+    if (total <= 0) return hipSuccess;
+    if ((total + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(copy_rows_kernel, dim3(unsigned((total + 255) / 256)), dim3(256), 0, s, dst, dst_stride, src,
+                       src_stride, width, total);
+    return hipGetLastError();
+}
 
 hipError_t launch_final_data_len_ranked(const uint8_t *data, int64_t obj_stride, int64_t len, int n_obj, int k,
                                         const int32_t *rank, unsigned long long *scratch, int32_t *status,

@@ -17,6 +17,20 @@ def test_library_exports_every_declared_symbol():
     assert sorted(_lib._SIGS) == syms
 
 
+def test_library_has_no_undefined_internal_symbols():
+    """Every rlnc:: function the engine calls is defined in the library (a shared object links with undefined
+    symbols and would only fail when loaded or called)."""
+    import shutil
+    import subprocess
+
+    from rlnc_amd import _lib
+
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True)
+    undefined = [ln.split()[-1] for ln in out.stdout.splitlines() if "_ZN4rlnc" in ln]
+    assert not undefined, undefined
+
+
 def test_status_names_follow_errors_rs():
     from rlnc_amd import _lib
     from rlnc_amd.errors import STATUS_NAMES, RLNCError
