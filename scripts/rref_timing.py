@@ -65,6 +65,8 @@ def main():
         line = {"case": name, "decode_path": path, "decode_ms_med": round(times[len(times) // 2], 4), "decode_ms_min": round(times[0], 4)}
         if os.environ.get("RLNC_RREF_PROFILE"):  # diagnostic library: cycles per piece / setup (object 0..2)
             line["phase_cycles_obj0_1"] = pst[:2, :8].cpu().tolist()
+            ent = pst[:, 4].cpu().numpy().astype(np.int64)
+            line["entry_ticks_10ns_rel"] = (ent - ent.min()).tolist()  # when each object's workgroup started
             line["phase_names"] = "row_init spare_copy forward normalise backward generic is_clean status"
         else:
             line["object_status"] = ost.cpu().tolist()
