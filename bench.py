@@ -213,9 +213,12 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the all-cores CPU baseline (one object each; the box's share is 16 cores per GPU)")
     ap.add_argument("--encode-only", action="store_true", help="diagnostic: time only the encode launch")
-    ap.add_argument("--pipeline", type=int, default=1,
+    ap.add_argument("--pipeline", type=int, default=2,
                     help="1: the decoder's elimination (reads only the coded pieces' coefficient headers, written "
-                         "first) runs on a second stream while the encode's data work runs; 0: strictly serial")
+                         "first) runs on a second stream while the encode's data work runs; 2: as 1, and successive "
+                         "steps overlap (two buffer sets: step i+1's encode runs beside step i's decode); 0: serial")
+    ap.add_argument("--breakdown-steps", type=int, default=24,
+                    help="--pipeline 2: steps of the pipeline-1 form run before the timed loop for the per-part times")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay each step as one captured HIP graph (the kernels of a step, launched together)")
     args = ap.parse_args()
@@ -300,7 +303,45 @@ def main():
         enc_events.append((e0, e1))
         dec_events.append((e1, e2))
 
-    run = step
+    # --pipeline 2: step i uses buffer set i % 2; its headers + elimination (side stream), encode data (launch
+    # stream) and decode data side (decode stream) wait only for step i-2's decode to release that set, so step
+    # i+1's encode fills the GPU beside step i's decode (no tail or launch gaps between the big kernels)
+    if args.pipeline == 2 and not args.encode_only:
+        sets = [dict(pieces=pieces, decoded=decoded, pst=piece_status, ost=object_status, dl=data_len, T=T, rank=rank)]
+        sets.append(dict(pieces=torch.empty_like(pieces), decoded=torch.empty_like(decoded),
+                         pst=torch.empty_like(piece_status), ost=torch.empty_like(object_status),
+                         dl=torch.empty_like(data_len), T=torch.empty_like(T), rank=torch.empty_like(rank)))
+        ctx_dec = rlnc_amd.Context(dist.local_rank)
+        ctx_dec.set_kernel_variant(args.variant, args.tile_rows)
+        s_dec = torch.cuda.Stream(dev)
+        ev_done = [torch.cuda.Event(), torch.cuda.Event()]
+        ev_enc = [torch.cuda.Event(), torch.cuda.Event()]
+        ev_el = [torch.cuda.Event(), torch.cuda.Event()]
+        count = [0]
+
+        def step2():
+            i = count[0]
+            count[0] += 1
+            bi = i % 2
+            S = sets[bi]
+            rec = S["pieces"][:, :m]
+            with torch.cuda.stream(side):
+                if i >= 2:
+                    side.wait_event(ev_done[bi])
+                batch.encode_batch_headers(coeffs, S["pieces"], ctx_side)
+                batch.decode_batch_eliminate(rec, k, S["T"], S["pst"], S["rank"], ctx_side)
+                ev_el[bi].record()
+            if i >= 2:
+                torch.cuda.current_stream().wait_event(ev_done[bi])
+            batch.encode_batch_data(src, coeffs, S["pieces"], ctx)
+            ev_enc[bi].record()
+            with torch.cuda.stream(s_dec):
+                s_dec.wait_event(ev_enc[bi])
+                s_dec.wait_event(ev_el[bi])
+                batch.decode_batch_apply(rec, k, S["T"], S["rank"], S["decoded"], S["ost"], S["dl"], ctx_dec)
+                ev_done[bi].record()
+
+    run = step2 if args.pipeline == 2 and not args.encode_only else step
     if args.graph:
         # eager warmup steps (they also give the per-kernel breakdown), then capture one step's launches into
         # a graph: the timed steps replay it, identical kernels and work, without per-launch host overhead
@@ -312,25 +353,39 @@ def main():
             encode_launches()
             decode_launches()
         run = g.replay
+    if run is not step and not args.graph:
+        # --pipeline 2: the per-part times (encode launch for the roofline, decode) come from pipeline-1 steps run
+        # before the timed loop (the first 6 discarded: clocks and caches settle): a kernel's own duration, not its
+        # overlap with the next step's kernels
+        for _ in range(args.breakdown_steps + 6):
+            step()
+        torch.cuda.synchronize()
     elapsed = timed_loop(run, args.steps, args.warmup, dist, torch.cuda.synchronize)
     torch.cuda.synchronize()
     skip = 0 if args.graph else args.warmup  # graph mode: the eager warmup steps carry the breakdown
+    def verified(vdec, vpst, vost):
+        # every full-rank object decodes to its source
+        pst, ost = vpst.cpu().numpy(), vost.cpu().numpy()
+        good = True
+        for o in range(B):
+            if (pst[o] == 0).sum() == k:
+                good = good and torch.equal(vdec[o], src[o])
+            else:
+                good = good and int(ost[o]) == 10  # NotAllPiecesReceivedYet (rank-deficient draw)
+        return good and bool((pst == 0).sum(axis=1).max() == k)
+
+    # correctness of what was timed: the last step's outputs (--pipeline 2: the last two steps', one per buffer set)
+    ok = True
+    if run is not step and not args.graph:  # --pipeline 2
+        for S in sets:
+            ok = ok and verified(S["decoded"], S["pst"], S["ost"])
+        skip = 6
+    elif not args.encode_only:
+        ok = verified(decoded, piece_status, object_status)
     timed_enc = enc_events[skip:]
     enc_ms = sum(a.elapsed_time(b) for a, b in timed_enc) / len(timed_enc)
     timed_dec = dec_events[skip:]
     dec_ms = sum(a.elapsed_time(b) for a, b in timed_dec) / len(timed_dec)
-
-    # correctness of what was timed (last step's outputs): every full-rank object decodes to its source
-    ok = True
-    if not args.encode_only:
-        pst = piece_status.cpu().numpy()
-        ost = object_status.cpu().numpy()
-        for o in range(B):
-            if (pst[o] == 0).sum() == k:
-                ok = ok and torch.equal(decoded[o], src[o])
-            else:
-                ok = ok and int(ost[o]) == 10  # NotAllPiecesReceivedYet (rank-deficient draw)
-        ok = ok and bool((pst == 0).sum(axis=1).max() == k)
 
     per_rank_bytes = step_bytes(B, k, L, n) if not args.encode_only else B * n * encode_counter(k, L)
     total_bytes = dist.allreduce(float(per_rank_bytes * args.steps), "sum")
@@ -353,6 +408,8 @@ def main():
         "traffic_source": traffic_src,
         "kernel": f"{KERNELS[variant]} (encode: {n} coded pieces x {B} objects per launch)",
         "kernel_ms": round(enc_ms, 4),
+        "kernel_ms_how": ("HIP events around the encode launch on its stream, in pipeline-1 steps (the elimination "
+                          "beside it, no other step's kernels)") if args.pipeline else "HIP events around the encode launch",
         "outputs_per_pass": n,
         "compulsory_bytes": enc_compulsory,
         "compulsory_GBps": round(enc_compulsory / (enc_ms * 1e-3) / 1e9, 1),
@@ -405,8 +462,9 @@ def main():
             "k": k, "piece_bytes": L, "coded_per_object": n, "decoded_from": m, "objects_per_gpu": B,
             "parallelism": f"objects sharded over {dist.world} rank(s), no data-path collective",
             "kernel_variant": variant,
-            "pipeline": "elimination on a side stream concurrent with the encode data work" if args.pipeline
-                        else "serial",
+            "pipeline": {0: "serial", 1: "elimination on a side stream concurrent with the encode data work",
+                         2: "elimination beside the encode data work, and step i+1's encode beside step i's decode "
+                            "(two buffer sets)"}[args.pipeline],
         },
         "roofline": roofline,
         "hbm_single_pass_encode": single,
