@@ -34,8 +34,14 @@ if fatal $rc; then exit $rc; fi
 
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   cd /tmp
+  # per-kernel durations of isolated launches (pipeline-1 steps: no overlap between steps), the roofline's source
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-      python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/prof.log" 2>&1
+      python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --pipeline 1 ${BENCH_ARGS:-} > "$OUT/prof.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"
   find "$OUT/prof" -name "*stats*" | head
+  if fatal $rc; then exit $rc; fi
+  # the default (cross-step pipelined) bench's timeline
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_p2" -o run --output-format csv -- \
+      python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/prof_p2.log" 2>&1
+  rc=$?; echo "rocprof (pipelined) rc=$rc"
 fi
