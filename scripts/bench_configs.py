@@ -10,7 +10,7 @@
 
 GiB/s in the reference's own counters (benches/full_rlnc_*.rs): encode (kL + k + L) per coded
 piece, decode k(k + L) per object, recode (n + 1)(k + L) per recoded piece.  HIP events around the launches on
-the launch stream, median of ROUNDS; every config's outputs are checked (decode: recovered source; recode:
+the launch stream (5 back-to-back calls per sample), median of ROUNDS; every config's outputs are checked (decode: recovered source; recode:
 decodes back).  One JSON line per config.
 """
 import json
@@ -22,18 +22,21 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 
 
-def timed(fn, rounds):
+def timed(fn, rounds, reps=5):
+    """Median over `rounds` of the mean time of `reps` back-to-back calls (steady clocks: a lone call after an
+    idle gap runs ~15 % slower while the GPU clock ramps up)."""
     import torch
 
     ts = []
     for r in range(rounds + 2):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        fn()
+        for _ in range(reps):
+            fn()
         b.record()
         torch.cuda.synchronize()
         if r >= 2:
-            ts.append(a.elapsed_time(b))
+            ts.append(a.elapsed_time(b) / reps)
     return sorted(ts)[len(ts) // 2]
 
 
