@@ -872,7 +872,8 @@ size_t bsj_scratch_bytes(const MatmulParams &p) {
 }
 
 // Address of the shared-set program's block table on the current device: one probe launch per device (the
-// code object does not move while the process runs).  Synchronous on `s` the first time only.
+// code object does not move while the process runs).  Synchronous on `s` the first time only; base = 0 when
+// that first time is inside a stream capture (the caller then takes the relative-offset program).
 static hipError_t bsj_shared_base(hipStream_t s, void *scratch, uint64_t &base) {
     static std::mutex mu;
     static uint64_t bases[64] = {};
@@ -881,7 +882,11 @@ static hipError_t bsj_shared_base(hipStream_t s, void *scratch, uint64_t &base) 
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     std::lock_guard<std::mutex> lock(mu);
+    base = 0;
     if (bases[dev] == 0) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if ((e = hipStreamIsCapturing(s, &cs)) != hipSuccess) return e;
+        if (cs != hipStreamCaptureStatusNone) return hipSuccess;
         MatmulParams q{};
         q.n_obj = 1;
         q.n_out = 1;
@@ -908,11 +913,13 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
     const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
     if (scratch == nullptr || scratch_bytes < bsj_scratch_bytes(p)) return hipErrorInvalidValue;
     if (total > 0x7FFFFFFFLL || p.n_obj > 65535) return hipErrorInvalidValue;
-    const bool abs = share && W == 4;  // the shared-set program calls absolute block addresses
+    bool abs = share && W == 4;  // the shared-set program calls absolute block addresses
     uint64_t base = 0;
     if (abs) {
         hipError_t e = bsj_shared_base(s, scratch, base);
         if (e != hipSuccess) return e;
+        abs = base != 0;  // first use inside a stream capture: the (bit-identical) variant-6 program this time
+        share = abs;
     }
     void *stream = scratch;
     const int64_t per_obj = int64_t(row_tiles) * p.n_in * tile_rows;

@@ -1,0 +1,58 @@
+"""GPU: the batch API under HIP-graph capture (bench.py --graph), including a capture that is the process's first
+use of the shared-set kernel (its one-time table-address probe cannot run inside a capture: that launch takes the
+bit-identical variant-6 program).  Runs in a child process so that the capture really is the first use.  Context
+workspaces must have grown before a capture (an eager call of the same shape), like torch's own warm-up rule."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import sys
+sys.path.insert(0, ROOT)
+import numpy as np
+import torch
+import rlnc_amd
+from rlnc_amd import batch
+
+ctx = rlnc_amd.Context(0)
+rng = np.random.default_rng(5)
+B, k, L, n = 3, 32, 3 * 4096 + 32, 40
+src = torch.from_numpy(rng.integers(0, 256, (B, k, L), dtype=np.uint8)).cuda()
+co = torch.from_numpy(rng.integers(0, 256, (B, n, k), dtype=np.uint8)).cuda()
+cap = torch.zeros((B, n, k + L), dtype=torch.uint8, device="cuda")
+# workspaces grow outside a capture (as torch's own warm-up rule): one eager call with variant 6, so that the
+# captured variant-7 call below is the first use of the shared-set kernel (its address probe is not yet done)
+ctx.set_kernel_variant(6)
+batch.encode_batch(src, co, cap, ctx)
+torch.cuda.synchronize()
+ctx.set_kernel_variant(7)
+cap.zero_()
+s = torch.cuda.Stream()
+with torch.cuda.stream(s):
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        batch.encode_batch(src, co, cap, ctx)
+g.replay()
+torch.cuda.synchronize()
+eager = torch.zeros_like(cap)
+batch.encode_batch(src, co, eager, ctx)
+torch.cuda.synchronize()
+assert torch.equal(cap, eager), "captured encode differs from eager"
+cap.zero_()
+g.replay()
+torch.cuda.synchronize()
+assert torch.equal(cap, eager), "replay differs"
+print("graph ok")
+"""
+
+
+def test_encode_batch_under_graph_capture_first_use():
+    r = subprocess.run([sys.executable, "-c", CHILD.replace("ROOT", repr(ROOT))], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "graph ok" in r.stdout
