@@ -95,6 +95,11 @@ SHARED_SGPRS = dict(S_SRC=68, S_IDX=70, S_DST=72, S_BASE=74, S_TGT=76, S_RET=78,
 LAST_VGPR_ALL, LAST_SGPR_ALL = 243, 87
 
 DIAG = set()
+# The shared program raises the wave priority (s_setprio) for the calls from PRIO_AT[0] on and drops it after
+# the next barrier: the wave finishing a row (which the other 3 waves of its workgroup wait for at the barrier) wins
+# issue over the co-resident wave of the other workgroup.  Calls 2.. at level 2: -2..4 % encode time (A/B in
+# profiles/r01_bsj_diag.txt, levels 1-3 and first calls 0/2/4/6 within noise of each other).  --prio K,L / --prio off.
+PRIO_AT = (2, 2)
 ALIGN = 0  # log2 alignment of the first block (--align)
 
 
@@ -346,6 +351,10 @@ def body_s(L, j):
     L += ["s_waitcnt vmcnt(1) lgkmcnt(0)",  # row j+2's DMA landed (row j+3's may fly); own set j + RB[j+1] done
           "s_barrier" if "snobar" not in DIAG else "s_nop 0",  # every wave's set of row j written, row j+2
           f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1"]                   # landed, row j+1's ring slot read by all
+    if PRIO_AT is not None:
+        L.append("s_setprio 0")
+    if "sprio2" in DIAG:
+        L.append("s_setprio 2")  # experiment: set building (what the other waves wait for next row) first
     for st in range(4):
         for q in range(4):
             r = G(st >> 1, st & 1, 4 * q)
@@ -362,6 +371,8 @@ def body_s(L, j):
     else:
         own_set(L, (j + 1) % 2, (j + 1) % 2)
     cur, nxt = S_ADDR[j % 2], S_ADDR[(j + 1) % 2]
+    if "sprio2" in DIAG:
+        L.append("s_setprio 0")
     L += [
         # the 16 set reads (LDS returns in order; 2 staging reads + 4 writes may fly)
         "s_waitcnt lgkmcnt(6)" if "snowait" not in DIAG else "s_nop 0",
@@ -377,6 +388,8 @@ def body_s(L, j):
             L += [f"v_bitop3_b32 v{ACC(0, g, o)}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])}, v{ACC(0, g, o)} bitop3:0x96"
                   for g in range(2) for o in range(8)]
             continue
+        if PRIO_AT is not None and i == PRIO_AT[0]:  # the calls closest to the next barrier at raised priority
+            L.append(f"s_setprio {PRIO_AT[1]}")
         # row i: M0 = its accumulator slot, then the call to the absolute address of block c (rows past
         # n_out have c = 0, whose block returns at once)
         L += [f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}",
@@ -517,7 +530,11 @@ def main():
     ap.add_argument("--diag", default="", help="comma list: novm, inline, absinline (timing diagnostics, wrong results)")
     ap.add_argument("--stride", type=int, default=BLOCK_BYTES, help="bytes per code block (>= 132, multiple of 4)")
     ap.add_argument("--align", type=int, default=0, help="log2 alignment of the block table")
+    ap.add_argument("--prio", default="", help="K,L: shared program's calls K.. of each row at s_setprio L")
     args = ap.parse_args()
+    global PRIO_AT
+    if args.prio:
+        PRIO_AT = None if args.prio == "off" else tuple(int(x) for x in args.prio.split(","))
     DIAG.update(x for x in args.diag.split(",") if x)
     assert args.stride >= BLOCK_BYTES and args.stride % 4 == 0
     BLOCK_BYTES, ALIGN = args.stride, args.align
