@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
 """bench.py — BASELINE.json metric: device-resident RLNC encode+decode GiB/s, k=32 × 1 MiB, 1/2/4/8 MI355X.
 
-One step = for each of --objects independent objects resident in HBM (16 × 32 MiB = 512 MiB of source per
-GPU, more than the 256 MiB Infinity Cache so source reads come from HBM):
+One step = for each of --objects independent objects resident in HBM (default 32 × 32 MiB = 1 GiB of source per
+GPU, more than the 256 MiB Infinity Cache so source reads come from HBM; larger launches run faster per object,
+profiles/r01_launch_size.txt):
   * encode: 32 source pieces × 1 MiB → 64 full coded pieces (BASELINE configs[1]); one kernel launch for all
     objects (librlnc_hip rlnc_encode_batch);
   * decode: feed the first 32 coded pieces of every object to a fresh Decoder (configs[2]): exact
-    diagonal-pivot elimination of the coefficient block per piece (host), then T × data on the device,
-    then the boundary-marker scan (rlnc_decode_batch).
+    diagonal-pivot elimination of the coefficient block per piece (device, gf_rref_batch_kernel), then
+    T × data on the device, then the boundary-marker scan (rlnc_decode_batch_eliminate / _apply).
 `value` = GiB/s in the reference's own byte counters (SURVEY.md §6 / BASELINE.md): per object
 64 × (k·L + k + L) for the 64 coded pieces (benches/full_rlnc_encoder.rs:111-113) + k·(k+L) for the decode
 (benches/full_rlnc_decoder.rs:118), summed over all ranks, ÷ the max-over-ranks wall time of the timed steps.
@@ -201,7 +202,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--objects", type=int, default=16, help="objects per GPU per step")
+    ap.add_argument("--objects", type=int, default=32, help="objects per GPU per step (32: profiles/r01_launch_size.txt)")
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--piece-bytes", type=int, default=1 << 20)
     ap.add_argument("--coded", type=int, default=64)
