@@ -92,7 +92,8 @@ CS_SLOT, CS_SET = 16384, 4096
 S_ADDR = (36, 52)
 SHARED_SGPRS = dict(S_SRC=68, S_IDX=70, S_DST=72, S_BASE=74, S_TGT=76, S_RET=78, S_INROW=80, S_OUTROW=81, S_CNT=82,
                     S_ROWS=83, S_T0=84, S_LDSW=85, S_NDMA=86, S_H=87)
-LAST_VGPR_ALL, LAST_SGPR_ALL = 243, 87
+S_CONS = 88  # 8-wave program: 1 for the consumer waves 4-7
+LAST_VGPR_ALL, LAST_SGPR_ALL = 243, 88
 
 DIAG = set()
 # The shared program raises the wave priority (s_setprio) for the calls from PRIO_AT[0] on and drops it after
@@ -345,9 +346,10 @@ def own_set(L, rb, cslot):
         L.append(f"ds_write_b128 %[ldscw], v[{OWN(4 * q)}:{OWN(4 * q) + 3}] offset:{cslot * CS_SLOT + q * 1024}")
 
 
-def body_s(L, j):
+def body_s(L, j, cons=False):
     """Source row j (j = the row index mod 6): sets of row j from LDS, row j + 2's staging read, row j + 4's
-    DMA, the own set of row j + 1, then row j's products."""
+    DMA, the own set of row j + 1, then row j's products.  cons (8-wave program): waves 4-7 (S_CONS != 0) only
+    read the sets and call; waves 0-3 stage, build and write the sets for all eight."""
     L += ["s_waitcnt vmcnt(1) lgkmcnt(0)",  # row j+2's DMA landed (row j+3's may fly); own set j + RB[j+1] done
           "s_barrier" if "snobar" not in DIAG else "s_nop 0",  # every wave's set of row j written, row j+2
           f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1"]                   # landed, row j+1's ring slot read by all
@@ -359,6 +361,8 @@ def body_s(L, j):
         for q in range(4):
             r = G(st >> 1, st & 1, 4 * q)
             L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsc] offset:{(j % 2) * CS_SLOT + st * CS_SET + q * 1024}")
+    if cons:
+        L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 20f"]
     for hh in range(2):
         r = RB(j % 2, 4 * hh)
         L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{((j + 2) % SLOTS) * 4096 + hh * 1024}")
@@ -376,6 +380,10 @@ def body_s(L, j):
     L += [
         # the 16 set reads (LDS returns in order; 2 staging reads + 4 writes may fly)
         "s_waitcnt lgkmcnt(6)" if "snowait" not in DIAG else "s_nop 0",
+    ]
+    if cons:  # consumer waves: no staging reads or set writes in flight, the 16 set reads are the last
+        L += ["s_branch 21f", "20:", "s_waitcnt lgkmcnt(0)", "21:"]
+    L += [
         f"s_load_dwordx16 s[{nxt}:{nxt + 15}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
         f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
         f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
@@ -397,17 +405,22 @@ def body_s(L, j):
     L.append("s_set_gpr_idx_off")
 
 
-def program_shared():
-    assert WAVES == 4
+def program_shared(cons=False):
+    assert WAVES == (8 if cons else 4)
     saved = {n: globals()[n] for n in SHARED_SGPRS}
     globals().update(SHARED_SGPRS)
     try:
-        return program_shared_body()
+        return program_shared_body(cons)
     finally:
         globals().update(saved)
 
 
-def program_shared_body():
+def program_shared_body(cons=False):
+    """cons: the 8-wave program (64-row tile): waves 0-3 are the 4-wave program's builders, waves 4-7 (rows
+    32-63) only read the sets and call.  It has no block table of its own: the offset kernel's absolute
+    addresses point into the 4-wave program's blocks (same register map, same return register)."""
+    if cons:
+        return program_shared8()
     L = [
         f"s_mov_b64 s[{S_SRC}:{S_SRC + 1}], %[src]",
         f"s_mov_b64 s[{S_IDX}:{S_IDX + 1}], %[idx]",
@@ -464,6 +477,55 @@ def program_shared_body():
     L.append("9:")
     blocks(L)
     L.append("8:")
+    return L
+
+
+def program_shared8():
+    L = [
+        f"s_mov_b64 s[{S_SRC}:{S_SRC + 1}], %[src]",
+        f"s_mov_b64 s[{S_IDX}:{S_IDX + 1}], %[idx]",
+        f"s_mov_b64 s[{S_DST}:{S_DST + 1}], %[dst]",
+        f"s_mov_b32 s{S_INROW}, %[in_row]",
+        f"s_mov_b32 s{S_OUTROW}, %[out_row]",
+        f"s_mov_b32 s{S_CNT}, %[n_in]",
+        f"s_sub_u32 s{S_NDMA}, %[n_in], 1",
+        f"s_mov_b32 s{S_H}, %[half]",
+        f"s_mov_b32 s{S_ROWS}, %[rows]",
+        f"s_mov_b32 s{S_CONS}, %[cons]",
+        f"v_mov_b32 v{V_MASK[0]}, 0xaaaaaaaa",
+        f"v_mov_b32 v{V_MASK[1]}, 0xcccccccc",
+        f"v_mov_b32 v{V_MASK[2]}, 0xf0f0f0f0",
+        f"s_mov_b32 s{S_LDSW}, %[ldsw]",
+        f"s_cmp_lg_u32 s{S_CONS}, 0",
+        "s_cbranch_scc1 22f",
+    ]
+    dmai = "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)
+    for slot in range(3):  # builders: rows 0, 1, 2 (clamped to the last row) into ring slots 0, 1, 2
+        if slot:
+            advance_s(L)
+        L += [f"s_add_u32 m0, s{S_LDSW}, {slot * 4096}", "s_nop 0", dmai]
+    L.append("22:")
+    L.append(f"s_load_dwordx16 s[{S_ADDR[0]}:{S_ADDR[0] + 15}], s[{S_IDX}:{S_IDX + 1}], 0")
+    L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
+    L.append(f"v_mov_b32 v{OWN(0)}, 0")
+    L += ["s_waitcnt vmcnt(1)", "s_barrier"]  # rows 0 and 1 landed (all builders; consumers have no loads)
+    L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 23f"]
+    for x in range(2):
+        for hh in range(2):
+            r = RB(x, 4 * hh)
+            L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{x * 4096 + hh * 1024}")
+    L += ["23:", "s_waitcnt lgkmcnt(0)", "s_barrier"]  # every builder has read slot 0: row 3 may overwrite it
+    L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 24f"]
+    advance_s(L)
+    L += [f"s_add_u32 m0, s{S_LDSW}, 0", "s_nop 0", dmai]
+    own_set(L, 0, 0)  # row 0's own set into set slot 0
+    L.append("24:")
+    L.append("1:")
+    for j in range(6):
+        body_s(L, j, cons=True)
+        L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f" if j < 5 else "s_cbranch_scc0 1b"]
+    L += ["3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    epilogue(L)
     return L
 
 
@@ -555,6 +617,10 @@ def main():
         STREAM_J_BYTES = WG_ROWS * 8  # 64-bit block addresses
         body_txt = "\\n\\t".join(program_shared())
         f.write(f'#define RLNC_BSJ_ASM_W4S "{body_txt}"\n')
+        WAVES, WG_ROWS = 8, NT * 8
+        STREAM_J_BYTES = WG_ROWS * 8
+        body_txt = "\\n\\t".join(program_shared(cons=True))
+        f.write(f'#define RLNC_BSJ_ASM_W8S "{body_txt}"\n')
         f.write(f"#define RLNC_BSJ_CSET_BYTES {2 * CS_SLOT}\n")
         f.write(f"#define RLNC_BSJ_CLOBBER_V {clob_v}\n")
         f.write(f'#define RLNC_BSJ_CLOBBER_S {clob_s}, "m0", "scc", "memory"\n')

@@ -802,7 +802,7 @@ __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, in
 template <int W, bool SHARE = false>
 __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const void *stream, int row_tiles,
                                                                int col_blocks, uint64_t *probe) {
-    static_assert(!SHARE || W == 4, "the shared-set program is generated for 4 waves");
+    static_assert(!SHARE || W == 4 || W == 8, "the shared-set programs are generated for 4 and 8 waves");
     constexpr int kTileRows = kBsjWaveRows * W;
     __shared__ __attribute__((aligned(16))) uint8_t ring[RLNC_BSJ_SLOTS * kBsjColBlock];
     __shared__ __attribute__((aligned(16))) uint8_t cset[SHARE ? RLNC_BSJ_CSET_BYTES : 16];
@@ -829,33 +829,41 @@ __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, c
                          ((int64_t(obj) * row_tiles + rt) * p.n_in * kTileRows + kBsjWaveRows * w) * kEntry;
     typedef __attribute__((address_space(3))) uint8_t lds_u8;
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)ring));  // addrspacecast
-    constexpr uint32_t kShare = kBsjColBlock / W;  // bytes of each row a wave moves into the ring
-    const uint32_t ldsw = __builtin_amdgcn_readfirstlane(ring_lds + kShare * uint32_t(w));
+    // W = 8 (shared): waves 0-3 stage the ring and build the sets exactly as in the 4-wave program, waves 4-7
+    // (cons = 1) only read the sets and call
+    constexpr int kStageWaves = (SHARE && W == 8) ? 4 : W;
+    const int ws = w % kStageWaves;
+    constexpr uint32_t kShare = kBsjColBlock / kStageWaves;  // bytes of each row a wave moves into the ring
+    const uint32_t ldsw = __builtin_amdgcn_readfirstlane(ring_lds + kShare * uint32_t(ws));
     const uint32_t ldsr = ring_lds + 16u * lane;
-    const uint32_t dmaoff = kShare * uint32_t(w) + 16u * lane;
+    const uint32_t dmaoff = kShare * uint32_t(ws) + 16u * lane;
     const uint32_t off = 16u * lane;
     const uint32_t ldsc = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)cset)) + 16u * lane;
-    const uint32_t ldscw = ldsc + 4096u * uint32_t(w);      // this wave's set (group w >> 1, half w & 1)
-    const uint32_t ldsrg = ldsr + 2048u * uint32_t(w >> 1);  // this wave's group of the ring chunk
-    const uint32_t half = uint32_t(w & 1);
+    const uint32_t ldscw = ldsc + 4096u * uint32_t(ws);      // this wave's set (group ws >> 1, half ws & 1)
+    const uint32_t ldsrg = ldsr + 2048u * uint32_t(ws >> 1);  // this wave's group of the ring chunk
+    const uint32_t half = uint32_t(ws & 1);
+    const uint32_t cons = uint32_t(w / kStageWaves);
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
 #define RLNC_BSJ_OPERANDS                                                                                            \
     : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),                           \
       [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw), [off] "v"(off), \
       [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr), [ldsc] "v"(ldsc), [ldscw] "v"(ldscw), [ldsrg] "v"(ldsrg),           \
-      [half] "s"(half), [probe] "s"(probe)                                                                        \
+      [half] "s"(half), [probe] "s"(probe), [cons] "s"(cons)                                                      \
     : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S
     if constexpr (W == 1) asm volatile(RLNC_BSJ_ASM_W1 : RLNC_BSJ_OPERANDS);
     if constexpr (W == 2) asm volatile(RLNC_BSJ_ASM_W2 : RLNC_BSJ_OPERANDS);
     if constexpr (W == 4 && !SHARE) asm volatile(RLNC_BSJ_ASM_W4 : RLNC_BSJ_OPERANDS);
     if constexpr (W == 4 && SHARE) asm volatile(RLNC_BSJ_ASM_W4S : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 8) asm volatile(RLNC_BSJ_ASM_W8S : RLNC_BSJ_OPERANDS);
 #undef RLNC_BSJ_OPERANDS
 #pragma clang diagnostic pop
 }
 
 // waves per workgroup: 8 output rows each, at most 4 (a 32-row tile), no more than the rows need
 inline int bsj_waves(int n_out) { return n_out <= 8 ? 1 : n_out <= 16 ? 2 : 4; }
+// wide = variant 8: 64-row tiles of 8 waves (shared program) above 32 output rows
+inline int bsj_waves(int n_out, bool wide) { return wide && n_out > 32 ? 8 : bsj_waves(n_out); }
 
 // Whole 4 KiB column blocks of 16-byte-aligned operands; the ragged tail goes to the perm kernel.
 bool bsj_eligible(const MatmulParams &p, bool aligned) {
@@ -863,8 +871,8 @@ bool bsj_eligible(const MatmulParams &p, bool aligned) {
            p.out_row < (int64_t(1) << 32);
 }
 
-size_t bsj_scratch_bytes(const MatmulParams &p) {
-    const int tile_rows = kBsjWaveRows * bsj_waves(p.n_out);
+size_t bsj_scratch_bytes(const MatmulParams &p, bool wide) {
+    const int tile_rows = kBsjWaveRows * bsj_waves(p.n_out, wide);
     const int64_t tiles = (p.n_out + tile_rows - 1) / tile_rows;
     // 8 bytes per entry (absolute addresses of the shared program, 4 otherwise) + one source: the main loop
     // loads the entries of the source after the last one
@@ -905,22 +913,24 @@ static hipError_t bsj_shared_base(hipStream_t s, void *scratch, uint64_t &base) 
 }
 
 hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full,
-                      bool share) {
+                      bool share, bool wide) {
     full = (p.width / kBsjColBlock) * kBsjColBlock;
-    const int W = bsj_waves(p.n_out), tile_rows = kBsjWaveRows * W;
-    const int row_tiles = (p.n_out + tile_rows - 1) / tile_rows;
-    const int col_blocks = int(full / kBsjColBlock);
-    const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
-    if (scratch == nullptr || scratch_bytes < bsj_scratch_bytes(p)) return hipErrorInvalidValue;
-    if (total > 0x7FFFFFFFLL || p.n_obj > 65535) return hipErrorInvalidValue;
-    bool abs = share && W == 4;  // the shared-set program calls absolute block addresses
+    if (scratch == nullptr || scratch_bytes < bsj_scratch_bytes(p, share && wide)) return hipErrorInvalidValue;
+    int W = bsj_waves(p.n_out, share && wide);
+    bool abs = share && W >= 4;  // the shared-set programs call absolute block addresses
     uint64_t base = 0;
     if (abs) {
         hipError_t e = bsj_shared_base(s, scratch, base);
         if (e != hipSuccess) return e;
         abs = base != 0;  // first use inside a stream capture: the (bit-identical) variant-6 program this time
         share = abs;
+        if (!abs) W = bsj_waves(p.n_out);
     }
+    const int tile_rows = kBsjWaveRows * W;
+    const int row_tiles = (p.n_out + tile_rows - 1) / tile_rows;
+    const int col_blocks = int(full / kBsjColBlock);
+    const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
+    if (total > 0x7FFFFFFFLL || p.n_obj > 65535) return hipErrorInvalidValue;
     void *stream = scratch;
     const int64_t per_obj = int64_t(row_tiles) * p.n_in * tile_rows;
     if ((per_obj + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
@@ -941,6 +951,9 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
     else if (W == 2)
         hipLaunchKernelGGL(gf_matmul_bsj_kernel<2>, dim3(unsigned(total)), dim3(128), 0, s, q, stream, row_tiles,
                            col_blocks, nullptr);
+    else if (W == 8)
+        hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true>), dim3(unsigned(total)), dim3(512), 0, s, q, stream,
+                           row_tiles, col_blocks, nullptr);
     else if (share)
         hipLaunchKernelGGL((gf_matmul_bsj_kernel<4, true>), dim3(unsigned(total)), dim3(256), 0, s, q, stream,
                            row_tiles, col_blocks, nullptr);
@@ -1105,18 +1118,20 @@ static bool matmul_aligned(const MatmulParams &p) {
 }
 
 size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v) {
-    if ((v != MatmulVariant::BitSliced && v != MatmulVariant::BitSlicedJump && v != MatmulVariant::BitSlicedJumpShared) ||
+    if ((v != MatmulVariant::BitSliced && v != MatmulVariant::BitSlicedJump && v != MatmulVariant::BitSlicedJumpShared &&
+         v != MatmulVariant::BitSlicedJumpShared8) ||
         p.n_out <= 0 || p.n_in <= 0 || p.n_obj <= 0)
         return 0;
     if (v == MatmulVariant::BitSliced) return bs_eligible(p, matmul_aligned(p)) ? bs_scratch_bytes(p) : 0;
-    return bsj_eligible(p, matmul_aligned(p)) ? bsj_scratch_bytes(p) : 0;
+    return bsj_eligible(p, matmul_aligned(p)) ? bsj_scratch_bytes(p, v == MatmulVariant::BitSlicedJumpShared8) : 0;
 }
 
 hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, void *scratch, size_t scratch_bytes) {
     if (p.n_out <= 0 || p.width <= 0 || p.n_obj <= 0) return hipSuccess;
     const bool aligned = matmul_aligned(p);
     if (p.n_in <= 0) return hipErrorInvalidValue;
-    const bool jump = v == MatmulVariant::BitSlicedJump || v == MatmulVariant::BitSlicedJumpShared;
+    const bool jump = v == MatmulVariant::BitSlicedJump || v == MatmulVariant::BitSlicedJumpShared ||
+                      v == MatmulVariant::BitSlicedJumpShared8;
     if (jump && aligned && p.n_out <= 3 && p.width >= kColBlock) {
         // one to three coded pieces per source pass: HBM-bound, streamed with deep prefetch
         const int64_t full = (p.width / kColBlock) * kColBlock;
@@ -1131,11 +1146,12 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
         return launch_matmul(t, s, MatmulVariant::Perm);
     }
     if (v == MatmulVariant::BitSliced || jump) {
-        const bool share = v == MatmulVariant::BitSlicedJumpShared;
+        const bool share = v == MatmulVariant::BitSlicedJumpShared || v == MatmulVariant::BitSlicedJumpShared8;
+        const bool wide = v == MatmulVariant::BitSlicedJumpShared8;
         v = MatmulVariant::Perm;  // whatever the bit-sliced kernels do not cover
         if (jump ? bsj_eligible(p, aligned) : bs_eligible(p, aligned)) {
             int64_t full = 0;
-            hipError_t e = jump ? launch_bsj(p, s, scratch, scratch_bytes, full, share)
+            hipError_t e = jump ? launch_bsj(p, s, scratch, scratch_bytes, full, share, wide)
                                 : launch_bs(p, s, scratch, scratch_bytes, full);
             if (e != hipSuccess || full == p.width) return e;
             MatmulParams t = p;

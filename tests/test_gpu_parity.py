@@ -68,7 +68,7 @@ SHAPES = [(1, 1, 1, 1), (1, 3, 17, 1), (2, 2, 16, 2), (3, 5, 4095, 1), (4, 32, 4
           (9, 40, 32768, 1), (1, 32, 8192 + 16, 2), (2, 7, 4096, 1), (3, 33, 12288 + 48, 2), (1, 70, 4096 * 5, 1)]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("n_out,n_in,W,nobj", SHAPES)
 def test_matmul(ctx, variant, n_out, n_in, W, nobj):
     from rlnc_amd import batch
@@ -97,7 +97,7 @@ BS_SHAPES = [(4, 1, 16384, 1), (5, 2, 16384 + 16, 2), (8, 32, 32768, 1), (9, 31,
              (3, 5, 16384, 1)]
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7])
+@pytest.mark.parametrize("variant", [5, 6, 7, 8])
 @pytest.mark.parametrize("n_out,n_in,W,nobj", BS_SHAPES)
 def test_matmul_bitsliced(ctx, variant, n_out, n_in, W, nobj):
     from rlnc_amd import batch
@@ -117,6 +117,51 @@ def test_matmul_bitsliced(ctx, variant, n_out, n_in, W, nobj):
         ctx.set_kernel_variant(DEFAULT_VARIANT, 0)
     for o in range(nobj):
         assert np.array_equal(got[o], np_matmul(coef[o], inp[o])), o
+
+
+# variant 8: 64-row tiles of 8 waves above 32 output rows (waves 4-7 read the sets built by waves 0-3)
+W8_SHAPES = [(33, 32, 4096, 1), (64, 32, 8192, 2), (65, 3, 4096 * 3 + 17, 1), (100, 17, 8192, 2), (128, 128, 4096, 1),
+             (40, 1, 4096, 3), (64, 64, 4096 * 4, 1)]
+
+
+@pytest.mark.parametrize("n_out,n_in,W,nobj", W8_SHAPES)
+def test_matmul_eight_wave_tiles(ctx, n_out, n_in, W, nobj):
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(n_out * 11 + n_in * 5 + W + nobj)
+    coef = rng.integers(0, 256, (nobj, n_out, n_in), dtype=np.uint8)
+    coef[:, 0, :] = 1
+    coef[:, -1, :] = 0
+    coef[:, 33 % n_out, : min(3, n_in)] = [0, 2, 0x80][: min(3, n_in)]
+    inp = rng.integers(0, 256, (nobj, n_in, W), dtype=np.uint8)
+    inp[:, 0, :256] = np.arange(256, dtype=np.uint8)
+    out = dev(np.zeros((nobj, n_out, W), np.uint8))
+    ctx.set_kernel_variant(8, 0)
+    try:
+        batch.matmul(dev(coef), dev(inp), out, ctx)
+        got = host(out)
+    finally:
+        ctx.set_kernel_variant(DEFAULT_VARIANT, 0)
+    for o in range(nobj):
+        assert np.array_equal(got[o], np_matmul(coef[o], inp[o])), o
+
+
+def test_matmul_every_coefficient_eight_waves(ctx):
+    """All 256 coefficients in a 64-row tile (64 rows x 4 sources), each against every byte value."""
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(257)
+    coef = np.arange(256, dtype=np.uint8).reshape(1, 64, 4)
+    inp = rng.integers(0, 256, (1, 4, 8192), dtype=np.uint8)
+    inp[0, :, :256] = np.arange(256, dtype=np.uint8)
+    out = dev(np.zeros((1, 64, 8192), np.uint8))
+    ctx.set_kernel_variant(8, 0)
+    try:
+        batch.matmul(dev(coef), dev(inp), out, ctx)
+        got = host(out)
+    finally:
+        ctx.set_kernel_variant(DEFAULT_VARIANT, 0)
+    assert np.array_equal(got[0], np_matmul(coef[0], inp[0]))
 
 
 @pytest.mark.parametrize("variant", [5, 6, 7])
