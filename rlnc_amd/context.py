@@ -51,12 +51,12 @@ class Context:
         one wave's registers (all exact; 2-4 exist for A/B)."""
         check(self.lib.rlnc_set_decode_path(self.h, int(path)), self.lib)
 
-    def set_kernel_variant(self, variant: int = 7, max_tile_rows: int = 0):
+    def set_kernel_variant(self, variant: int = 8, max_tile_rows: int = 0):
         """GF(2^8) matmul variant (include/rlnc_hip.h): 7 = bit-sliced, one code block per coefficient, plane
-        combinations built once per workgroup and shared through LDS (default), 6 = the same without sharing,
+        combinations built once per workgroup and shared through LDS, 6 = the same without sharing,
         5 = bit-sliced with register-indexed XORs, 0 = perm, 1 = nibble (the reference's 4-bit tables,
         ablation), 2 = perm3, 3/4 = wide2/wide4, 8 = as 7 with 64-row tiles of 8 waves above 32 output rows
-        (waves 4-7 only read the shared combinations).  All are bit-identical."""
+        (waves 4-7 only read the shared combinations; a barrier every second row; the default).  All are bit-identical."""
         check(self.lib.rlnc_set_kernel_variant(self.h, int(variant), int(max_tile_rows)), self.lib)
 
 

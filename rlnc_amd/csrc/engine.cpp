@@ -102,7 +102,7 @@ struct rlnc_context {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
-    rlnc::MatmulVariant variant = rlnc::MatmulVariant::BitSlicedJumpShared;
+    rlnc::MatmulVariant variant = rlnc::MatmulVariant::BitSlicedJumpShared8;
     int max_tile_rows = 0;
     int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination,
                           // 3 device elimination with the clean state on LDS, 4 ... on one wave's

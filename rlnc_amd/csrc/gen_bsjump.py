@@ -480,6 +480,52 @@ def program_shared_body(cons=False):
     return L
 
 
+# 8-wave program: one workgroup per CU leaves LDS for SLOTS8 ring slots and CSLOTS8 set slots, so the builders run
+# two rows ahead (staging read of row j + 3, set of row j + 2, DMA of row j + 6 during row j) and the workgroup
+# meets at a barrier every second row (even j) instead of every row.
+SLOTS8, CSLOTS8 = 6, 4
+
+
+def body_s8(L, j):
+    """Source row j (j = the row index mod 12): sets of row j, then -- builders only -- the staging read of row
+    j + 3, the DMA of row j + 6 and the own set of row j + 2; then row j's products.  Barrier at even j only:
+    it orders the set writes of rows j, j + 1 (made during rows j - 2, j - 1) before their reads, the ring
+    landing of rows <= j + 4 before their staging reads, and every read of a slot before its reuse."""
+    L.append("s_waitcnt vmcnt(1) lgkmcnt(0)")  # rows <= j+4 landed (j+5 may fly); own LDS ops + addresses done
+    if j % 2 == 0:
+        L.append("s_barrier")
+    L.append(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
+    if PRIO_AT is not None:
+        L.append("s_setprio 0")
+    for st in range(4):
+        for q in range(4):
+            r = G(st >> 1, st & 1, 4 * q)
+            L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsc] offset:{(j % CSLOTS8) * CS_SLOT + st * CS_SET + q * 1024}")
+    L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 20f"]
+    for hh in range(2):  # row j+3 into RB[(j+1) % 2] (row j+1's set was built from it during row j-1)
+        r = RB((j + 1) % 2, 4 * hh)
+        L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{((j + 3) % SLOTS8) * 4096 + hh * 1024}")
+    advance_s(L)
+    L += [f"s_add_u32 m0, s{S_LDSW}, {((j + 6) % SLOTS8) * 4096}", "s_nop 0",
+          "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)]  # row j+6
+    own_set(L, j % 2, (j + 2) % CSLOTS8)  # row j+2's set from RB[j % 2]
+    L += ["s_waitcnt lgkmcnt(6)",  # the 16 set reads (2 staging reads + 4 set writes may fly)
+          "s_branch 21f", "20:", "s_waitcnt lgkmcnt(0)", "21:"]
+    cur, nxt = S_ADDR[j % 2], S_ADDR[(j + 1) % 2]
+    L += [
+        f"s_load_dwordx16 s[{nxt}:{nxt + 15}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
+        f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
+        f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
+        "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)",
+    ]
+    for i in range(NT):
+        if PRIO_AT is not None and i == PRIO_AT[0]:
+            L.append(f"s_setprio {PRIO_AT[1]}")
+        L += [f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}",
+              f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{cur + 2 * i}:{cur + 2 * i + 1}]"]
+    L.append("s_set_gpr_idx_off")
+
+
 def program_shared8():
     L = [
         f"s_mov_b64 s[{S_SRC}:{S_SRC + 1}], %[src]",
@@ -500,7 +546,7 @@ def program_shared8():
         "s_cbranch_scc1 22f",
     ]
     dmai = "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)
-    for slot in range(3):  # builders: rows 0, 1, 2 (clamped to the last row) into ring slots 0, 1, 2
+    for slot in range(SLOTS8):  # builders: rows 0..5 (clamped to the last row) into ring slots 0..5
         if slot:
             advance_s(L)
         L += [f"s_add_u32 m0, s{S_LDSW}, {slot * 4096}", "s_nop 0", dmai]
@@ -508,22 +554,24 @@ def program_shared8():
     L.append(f"s_load_dwordx16 s[{S_ADDR[0]}:{S_ADDR[0] + 15}], s[{S_IDX}:{S_IDX + 1}], 0")
     L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
     L.append(f"v_mov_b32 v{OWN(0)}, 0")
-    L += ["s_waitcnt vmcnt(1)", "s_barrier"]  # rows 0 and 1 landed (all builders; consumers have no loads)
+    L += ["s_waitcnt vmcnt(3)", "s_barrier"]  # rows 0-2 landed (all builders; consumers have no loads)
     L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 23f"]
-    for x in range(2):
+    for x in range(2):  # rows 0, 1 into RB[0], RB[1]
         for hh in range(2):
             r = RB(x, 4 * hh)
             L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{x * 4096 + hh * 1024}")
-    L += ["23:", "s_waitcnt lgkmcnt(0)", "s_barrier"]  # every builder has read slot 0: row 3 may overwrite it
-    L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 24f"]
-    advance_s(L)
-    L += [f"s_add_u32 m0, s{S_LDSW}, 0", "s_nop 0", dmai]
-    own_set(L, 0, 0)  # row 0's own set into set slot 0
-    L.append("24:")
+    L.append("s_waitcnt lgkmcnt(0)")
+    own_set(L, 0, 0)  # row 0's set into set slot 0
+    for hh in range(2):  # row 2 into RB[0]
+        r = RB(0, 4 * hh)
+        L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{2 * 4096 + hh * 1024}")
+    L.append("s_waitcnt lgkmcnt(0)")  # row 0's set writes have read OWN
+    own_set(L, 1, 1)  # row 1's set into set slot 1
+    L += ["23:", "s_waitcnt lgkmcnt(0)"]
     L.append("1:")
-    for j in range(6):
-        body_s(L, j, cons=True)
-        L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f" if j < 5 else "s_cbranch_scc0 1b"]
+    for j in range(12):
+        body_s8(L, j)
+        L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f" if j < 11 else "s_cbranch_scc0 1b"]
     L += ["3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
     epilogue(L)
     return L
@@ -621,6 +669,8 @@ def main():
         STREAM_J_BYTES = WG_ROWS * 8
         body_txt = "\\n\\t".join(program_shared(cons=True))
         f.write(f'#define RLNC_BSJ_ASM_W8S "{body_txt}"\n')
+        f.write(f"#define RLNC_BSJ_SLOTS8 {SLOTS8}\n")
+        f.write(f"#define RLNC_BSJ_CSET_BYTES8 {CSLOTS8 * CS_SLOT}\n")
         f.write(f"#define RLNC_BSJ_CSET_BYTES {2 * CS_SLOT}\n")
         f.write(f"#define RLNC_BSJ_CLOBBER_V {clob_v}\n")
         f.write(f'#define RLNC_BSJ_CLOBBER_S {clob_s}, "m0", "scc", "memory"\n')

@@ -804,8 +804,9 @@ __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, c
                                                                int col_blocks, uint64_t *probe) {
     static_assert(!SHARE || W == 4 || W == 8, "the shared-set programs are generated for 4 and 8 waves");
     constexpr int kTileRows = kBsjWaveRows * W;
-    __shared__ __attribute__((aligned(16))) uint8_t ring[RLNC_BSJ_SLOTS * kBsjColBlock];
-    __shared__ __attribute__((aligned(16))) uint8_t cset[SHARE ? RLNC_BSJ_CSET_BYTES : 16];
+    // W = 8: one workgroup per CU, so a deeper ring and four set slots (the builders run two rows ahead)
+    __shared__ __attribute__((aligned(16))) uint8_t ring[(W == 8 ? RLNC_BSJ_SLOTS8 : RLNC_BSJ_SLOTS) * kBsjColBlock];
+    __shared__ __attribute__((aligned(16))) uint8_t cset[SHARE ? (W == 8 ? RLNC_BSJ_CSET_BYTES8 : RLNC_BSJ_CSET_BYTES) : 16];
     int rt, cb, obj;
     decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
     const int row0 = rt * kTileRows;

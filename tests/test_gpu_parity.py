@@ -12,7 +12,7 @@ from tests.gpu_util import MUL, dev, host, np_matmul
 
 pytestmark = pytest.mark.gpu
 
-DEFAULT_VARIANT = 7  # rlnc_context default (bit-sliced jump with shared combinations, perm for the rest)
+DEFAULT_VARIANT = 8  # rlnc_context default (bit-sliced jump with shared combinations, 8-wave tiles above 32 rows)
 
 S = ["Ok", "CodingVectorLengthMismatch", "DataLengthMismatch", "PieceCountZero", "DataLengthZero",
      "PieceLengthZero", "NotEnoughPiecesToRecode", "PieceLengthTooShort", "PieceNotUseful", "ReceivedAllPieces",
