@@ -209,7 +209,7 @@ def main():
     ap.add_argument("--piece-bytes", type=int, default=1 << 20)
     ap.add_argument("--coded", type=int, default=64)
     ap.add_argument("--decode-from", type=int, default=32)
-    ap.add_argument("--variant", type=int, default=8, help="matmul kernel variant: 8 as 7 with 64-row tiles of 8 waves above 32 output rows and a barrier every second row (default), 7 bit-sliced, one code block per coefficient, combinations shared through LDS, 6 the same without sharing, 5 bit-sliced relative XOR, 0 perm, 1 nibble-LDS, 2 perm3, 3/4 wide")
+    ap.add_argument("--variant", type=int, default=8, help="matmul kernel variant: 8 as 7 with 64-row tiles of 8 waves above 32 output rows and a barrier every third row (default), 7 bit-sliced, one code block per coefficient, combinations shared through LDS, 6 the same without sharing, 5 bit-sliced relative XOR, 0 perm, 1 nibble-LDS, 2 perm3, 3/4 wide")
     ap.add_argument("--tile-rows", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

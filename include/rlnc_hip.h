@@ -110,8 +110,8 @@ int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc);
  *   7 = bitsliced-jump-shared  as 6; in 32-row tiles each of the 4 waves builds one quarter of every source
  *                  row's plane combinations and the quarters are exchanged through LDS
  *   8 = bitsliced-jump-shared-8w  as 7; above 32 output rows, 64-row tiles of 8 waves (one workgroup per CU):
- *                  waves 0-3 stage the source and build the combinations two rows ahead, waves 4-7 only read
- *                  them and call; a barrier every second row -- the default
+ *                  waves 0-3 stage the source and build the combinations three rows ahead, waves 4-7 only
+ *                  read them and call; a barrier every third row -- the default
  * max_tile_rows caps the output rows per launch/workgroup (0 = automatic, else 1/2/4/8/16/32). */
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows);
 /* Where rlnc_decode_batch runs the coefficient elimination: 0 = auto (device when it fits LDS, default),

@@ -56,7 +56,7 @@ class Context:
         combinations built once per workgroup and shared through LDS, 6 = the same without sharing,
         5 = bit-sliced with register-indexed XORs, 0 = perm, 1 = nibble (the reference's 4-bit tables,
         ablation), 2 = perm3, 3/4 = wide2/wide4, 8 = as 7 with 64-row tiles of 8 waves above 32 output rows
-        (waves 4-7 only read the shared combinations; a barrier every second row; the default).  All are bit-identical."""
+        (waves 4-7 only read the shared combinations; a barrier every third row; the default).  All are bit-identical."""
         check(self.lib.rlnc_set_kernel_variant(self.h, int(variant), int(max_tile_rows)), self.lib)
 
 

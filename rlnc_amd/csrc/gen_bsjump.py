@@ -342,8 +342,9 @@ def own_set(L, rb, cslot):
         L.append("s_branch 6f" if h == 0 else "6:")
         if h == 0:
             L.append("4:")
+    sfx, base = cslot_addr(cslot)
     for q in range(4):
-        L.append(f"ds_write_b128 %[ldscw], v[{OWN(4 * q)}:{OWN(4 * q) + 3}] offset:{cslot * CS_SLOT + q * 1024}")
+        L.append(f"ds_write_b128 %[ldscw{sfx}], v[{OWN(4 * q)}:{OWN(4 * q) + 3}] offset:{base + q * 1024}")
 
 
 def body_s(L, j, cons=False):
@@ -480,35 +481,57 @@ def program_shared_body(cons=False):
     return L
 
 
-# 8-wave program: one workgroup per CU leaves LDS for SLOTS8 ring slots and CSLOTS8 set slots, so the builders run
-# two rows ahead (staging read of row j + 3, set of row j + 2, DMA of row j + 6 during row j) and the workgroup
-# meets at a barrier every second row (even j) instead of every row.
-SLOTS8, CSLOTS8 = 6, 4
+# 8-wave program: one workgroup per CU leaves LDS for SLOTS8 ring slots and CSLOTS8 = 2 BAR8 set slots, so the
+# builders run BAR8 rows ahead (staging read of row j + BAR8 + 1, set of row j + BAR8, DMA of row j + DMA8 during
+# row j) and the workgroup meets at a barrier every BAR8-th row instead of every row.  Conditions (vmcnt(1) at
+# every row top): DMA8 >= 2 BAR8 + 2 (rows <= x + 2 BAR8 landed at barrier x), SLOTS8 >= DMA8 - 1 (a ring slot is
+# refilled only after a barrier that follows its staging reads); set slot r % CSLOTS8 is rewritten BAR8 rows after
+# its last read, with one barrier in between.  BAR8 = 2: DMA8 = SLOTS8 = 6 (88 KiB); BAR8 = 3: DMA8 = 8,
+# SLOTS8 = 12 (144 KiB; set slots 4-5 through the second base, ds offsets are 16-bit).
+BAR8 = 3
+DMA8 = SLOTS8 = CSLOTS8 = 0
+# no wave priority in the 8-wave program (its consumer waves have no set building to overtake): -0.8 % encode
+# time against calls 2.. at level 2 (profiles/r01_launch_size.txt)
+PRIO8 = None
+
+
+def set_bar8(b):
+    global BAR8, DMA8, SLOTS8, CSLOTS8
+    BAR8, DMA8, SLOTS8, CSLOTS8 = b, 2 * b + 2, (6 if b == 2 else 12), 2 * b
+
+
+set_bar8(3)
+
+
+def cslot_addr(slot):  # (base operand, offset) of set slot `slot` for reads / the wave's own write
+    return ("", slot * CS_SLOT) if slot < 4 else ("2", (slot - 4) * CS_SLOT)
 
 
 def body_s8(L, j):
-    """Source row j (j = the row index mod 12): sets of row j, then -- builders only -- the staging read of row
-    j + 3, the DMA of row j + 6 and the own set of row j + 2; then row j's products.  Barrier at even j only:
-    it orders the set writes of rows j, j + 1 (made during rows j - 2, j - 1) before their reads, the ring
-    landing of rows <= j + 4 before their staging reads, and every read of a slot before its reuse."""
-    L.append("s_waitcnt vmcnt(1) lgkmcnt(0)")  # rows <= j+4 landed (j+5 may fly); own LDS ops + addresses done
-    if j % 2 == 0:
+    """Source row j (j = the row index mod the unroll): sets of row j, then -- builders only -- the staging read of
+    row j + BAR8 + 1, the DMA of row j + DMA8 and the own set of row j + BAR8; then row j's products.  Barrier
+    when j % BAR8 == 0: it orders the set writes of rows j .. j + BAR8 - 1 before their reads, the ring landing of
+    rows <= j + 2 BAR8 before their staging reads and every read of a slot before its reuse."""
+    L.append("s_waitcnt vmcnt(1) lgkmcnt(0)")  # rows <= j+DMA8-2 landed; own LDS ops + addresses done
+    if j % BAR8 == 0:
         L.append("s_barrier")
     L.append(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
-    if PRIO_AT is not None:
+    if PRIO8 is not None:
         L.append("s_setprio 0")
+    sfx, base = cslot_addr(j % CSLOTS8)
     for st in range(4):
         for q in range(4):
             r = G(st >> 1, st & 1, 4 * q)
-            L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsc] offset:{(j % CSLOTS8) * CS_SLOT + st * CS_SET + q * 1024}")
+            L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsc{sfx}] offset:{base + st * CS_SET + q * 1024}")
     L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 20f"]
-    for hh in range(2):  # row j+3 into RB[(j+1) % 2] (row j+1's set was built from it during row j-1)
-        r = RB((j + 1) % 2, 4 * hh)
-        L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{((j + 3) % SLOTS8) * 4096 + hh * 1024}")
+    nx = j + BAR8 + 1  # staged now into RB[nx % 2] (it held row nx - 2, whose set was built during row j - 1)
+    for hh in range(2):
+        r = RB(nx % 2, 4 * hh)
+        L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{(nx % SLOTS8) * 4096 + hh * 1024}")
     advance_s(L)
-    L += [f"s_add_u32 m0, s{S_LDSW}, {((j + 6) % SLOTS8) * 4096}", "s_nop 0",
-          "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)]  # row j+6
-    own_set(L, j % 2, (j + 2) % CSLOTS8)  # row j+2's set from RB[j % 2]
+    L += [f"s_add_u32 m0, s{S_LDSW}, {((j + DMA8) % SLOTS8) * 4096}", "s_nop 0",
+          "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)]  # row j + DMA8
+    own_set(L, (j + BAR8) % 2, (j + BAR8) % CSLOTS8)  # row j + BAR8's set
     L += ["s_waitcnt lgkmcnt(6)",  # the 16 set reads (2 staging reads + 4 set writes may fly)
           "s_branch 21f", "20:", "s_waitcnt lgkmcnt(0)", "21:"]
     cur, nxt = S_ADDR[j % 2], S_ADDR[(j + 1) % 2]
@@ -519,8 +542,8 @@ def body_s8(L, j):
         "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)",
     ]
     for i in range(NT):
-        if PRIO_AT is not None and i == PRIO_AT[0]:
-            L.append(f"s_setprio {PRIO_AT[1]}")
+        if PRIO8 is not None and i == PRIO8[0]:
+            L.append(f"s_setprio {PRIO8[1]}")
         L += [f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}",
               f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{cur + 2 * i}:{cur + 2 * i + 1}]"]
     L.append("s_set_gpr_idx_off")
@@ -546,7 +569,7 @@ def program_shared8():
         "s_cbranch_scc1 22f",
     ]
     dmai = "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)
-    for slot in range(SLOTS8):  # builders: rows 0..5 (clamped to the last row) into ring slots 0..5
+    for slot in range(DMA8):  # builders: rows 0 .. DMA8 - 1 (clamped to the last row) into ring slots
         if slot:
             advance_s(L)
         L += [f"s_add_u32 m0, s{S_LDSW}, {slot * 4096}", "s_nop 0", dmai]
@@ -554,24 +577,26 @@ def program_shared8():
     L.append(f"s_load_dwordx16 s[{S_ADDR[0]}:{S_ADDR[0] + 15}], s[{S_IDX}:{S_IDX + 1}], 0")
     L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
     L.append(f"v_mov_b32 v{OWN(0)}, 0")
-    L += ["s_waitcnt vmcnt(3)", "s_barrier"]  # rows 0-2 landed (all builders; consumers have no loads)
+    L += [f"s_waitcnt vmcnt({DMA8 - 1 - BAR8})", "s_barrier"]  # rows 0..BAR8 landed (consumers have no loads)
     L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 23f"]
     for x in range(2):  # rows 0, 1 into RB[0], RB[1]
         for hh in range(2):
             r = RB(x, 4 * hh)
             L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{x * 4096 + hh * 1024}")
     L.append("s_waitcnt lgkmcnt(0)")
-    own_set(L, 0, 0)  # row 0's set into set slot 0
-    for hh in range(2):  # row 2 into RB[0]
-        r = RB(0, 4 * hh)
-        L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{2 * 4096 + hh * 1024}")
-    L.append("s_waitcnt lgkmcnt(0)")  # row 0's set writes have read OWN
-    own_set(L, 1, 1)  # row 1's set into set slot 1
+    for r in range(BAR8):  # the sets of rows 0 .. BAR8 - 1; RB[BAR8 % 2] ends with row BAR8
+        own_set(L, r % 2, r)
+        if r + 2 <= BAR8:
+            for hh in range(2):
+                x = RB(r % 2, 4 * hh)
+                L.append(f"ds_read_b128 v[{x}:{x + 3}], %[ldsrg] offset:{(r + 2) * 4096 + hh * 1024}")
+        L.append("s_waitcnt lgkmcnt(0)")  # the set writes have read OWN; the staged row is in
     L += ["23:", "s_waitcnt lgkmcnt(0)"]
     L.append("1:")
-    for j in range(12):
+    unroll = 12  # lcm of BAR8, CSLOTS8, SLOTS8 and the two RB / address buffers (12 for BAR8 = 2 and 3)
+    for j in range(unroll):
         body_s8(L, j)
-        L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f" if j < 11 else "s_cbranch_scc0 1b"]
+        L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f" if j < unroll - 1 else "s_cbranch_scc0 1b"]
     L += ["3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
     epilogue(L)
     return L
@@ -640,12 +665,17 @@ def main():
     ap.add_argument("--diag", default="", help="comma list: novm, inline, absinline (timing diagnostics, wrong results)")
     ap.add_argument("--stride", type=int, default=BLOCK_BYTES, help="bytes per code block (>= 132, multiple of 4)")
     ap.add_argument("--align", type=int, default=0, help="log2 alignment of the block table")
+    ap.add_argument("--bar8", type=int, default=3, choices=(2, 3), help="8-wave program: a barrier every N rows")
+    ap.add_argument("--prio8", default="off", help="K,L: 8-wave program's calls K.. of each row at s_setprio L")
     ap.add_argument("--prio", default="", help="K,L: shared program's calls K.. of each row at s_setprio L")
     args = ap.parse_args()
     global PRIO_AT
     if args.prio:
         PRIO_AT = None if args.prio == "off" else tuple(int(x) for x in args.prio.split(","))
     DIAG.update(x for x in args.diag.split(",") if x)
+    set_bar8(args.bar8)
+    global PRIO8
+    PRIO8 = None if args.prio8 == "off" else tuple(int(x) for x in args.prio8.split(","))
     assert args.stride >= BLOCK_BYTES and args.stride % 4 == 0
     BLOCK_BYTES, ALIGN = args.stride, args.align
     clob_v = ", ".join(f'"v{r}"' for r in range(LAST_VGPR_ALL + 1))

@@ -804,7 +804,7 @@ __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, c
                                                                int col_blocks, uint64_t *probe) {
     static_assert(!SHARE || W == 4 || W == 8, "the shared-set programs are generated for 4 and 8 waves");
     constexpr int kTileRows = kBsjWaveRows * W;
-    // W = 8: one workgroup per CU, so a deeper ring and four set slots (the builders run two rows ahead)
+    // W = 8: one workgroup per CU, so a deeper ring and 2 BAR8 set slots (the builders run BAR8 rows ahead)
     __shared__ __attribute__((aligned(16))) uint8_t ring[(W == 8 ? RLNC_BSJ_SLOTS8 : RLNC_BSJ_SLOTS) * kBsjColBlock];
     __shared__ __attribute__((aligned(16))) uint8_t cset[SHARE ? (W == 8 ? RLNC_BSJ_CSET_BYTES8 : RLNC_BSJ_CSET_BYTES) : 16];
     int rt, cb, obj;
@@ -850,7 +850,8 @@ __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, c
     : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),                           \
       [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw), [off] "v"(off), \
       [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr), [ldsc] "v"(ldsc), [ldscw] "v"(ldscw), [ldsrg] "v"(ldsrg),           \
-      [half] "s"(half), [probe] "s"(probe), [cons] "s"(cons)                                                      \
+      [half] "s"(half), [probe] "s"(probe), [cons] "s"(cons), [ldsc2] "v"(ldsc + 65536u),                        \
+      [ldscw2] "v"(ldscw + 65536u)                                                                                \
     : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S
     if constexpr (W == 1) asm volatile(RLNC_BSJ_ASM_W1 : RLNC_BSJ_OPERANDS);
     if constexpr (W == 2) asm volatile(RLNC_BSJ_ASM_W2 : RLNC_BSJ_OPERANDS);

@@ -38,7 +38,7 @@ enum class MatmulVariant : int {
     BitSlicedJump = 6,
     BitSlicedJumpShared = 7,  // 6 with each row's combination sets built once per workgroup (4-wave tiles)
     BitSlicedJumpShared8 = 8  // 7 with 64-row tiles of 8 waves (n_out > 32): waves 4-7 only read the sets and call,
-                              // the builders run two rows ahead, one barrier per two rows (the default)
+                              // the builders run three rows ahead, one barrier per three rows (the default)
 };
 
 // Device scratch the BitSliced variant needs for its coefficient-index stream (0 for the others, and for
