@@ -48,6 +48,8 @@ def main():
 
     rounds = int(os.environ.get("ROUNDS", "6"))
     ctx = rlnc_amd.Context(0)
+    if os.environ.get("VARIANT"):  # A/B: another matmul kernel variant (default: the context's)
+        ctx.set_kernel_variant(int(os.environ["VARIANT"]), 0)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
     g.manual_seed(11)
