@@ -524,6 +524,8 @@ def body_s8(L, j):
             r = G(st >> 1, st & 1, 4 * q)
             L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsc{sfx}] offset:{base + st * CS_SET + q * 1024}")
     L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 20f"]
+    if "bprio" in DIAG:  # experiment: builders at raised priority while staging and building the sets
+        L.append("s_setprio 1")
     nx = j + BAR8 + 1  # staged now into RB[nx % 2] (it held row nx - 2, whose set was built during row j - 1)
     for hh in range(2):
         r = RB(nx % 2, 4 * hh)
@@ -532,6 +534,8 @@ def body_s8(L, j):
     L += [f"s_add_u32 m0, s{S_LDSW}, {((j + DMA8) % SLOTS8) * 4096}", "s_nop 0",
           "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)]  # row j + DMA8
     own_set(L, (j + BAR8) % 2, (j + BAR8) % CSLOTS8)  # row j + BAR8's set
+    if "bprio" in DIAG:
+        L.append("s_setprio 0")
     L += ["s_waitcnt lgkmcnt(6)",  # the 16 set reads (2 staging reads + 4 set writes may fly)
           "s_branch 21f", "20:", "s_waitcnt lgkmcnt(0)", "21:"]
     cur, nxt = S_ADDR[j % 2], S_ADDR[(j + 1) % 2]
