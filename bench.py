@@ -1,26 +1,36 @@
 #!/usr/bin/env python3
 """bench.py — BASELINE.json metric: device-resident RLNC encode+decode GiB/s, k=32 × 1 MiB, 1/2/4/8 MI355X.
 
-One step = for each of --objects independent objects resident in HBM (default 32 × 32 MiB = 1 GiB of source per
-GPU, more than the 256 MiB Infinity Cache so source reads come from HBM; larger launches run faster per object,
-profiles/r01_launch_size.txt):
-  * encode: 32 source pieces × 1 MiB → 64 full coded pieces (BASELINE configs[1]); one kernel launch for all
-    objects (librlnc_hip rlnc_encode_batch);
-  * decode: feed the first 32 coded pieces of every object to a fresh Decoder (configs[2]): exact
-    diagonal-pivot elimination of the coefficient block per piece (device, gf_rref_batch_kernel), then
-    T × data on the device, then the boundary-marker scan (rlnc_decode_batch_eliminate / _apply).
+Workloads (--workload):
+  config2 (default; the metric's own shape, weak scaling): per GPU per step, --objects independent objects
+    resident in HBM (default 32 × 32 MiB = 1 GiB of source, more than the 256 MiB Infinity Cache so source reads
+    come from HBM; larger launches run faster per object, profiles/r01_launch_size.txt):
+      * encode: 32 source pieces × 1 MiB → 64 full coded pieces (BASELINE configs[1]); one kernel launch for all
+        objects (librlnc_hip rlnc_encode_batch);
+      * decode: feed the first 32 coded pieces of every object to a fresh Decoder (configs[2]): exact
+        diagonal-pivot elimination of the coefficient block per piece (device, gf_rref_batch_kernel), then
+        T × data on the device, then the boundary-marker scan (rlnc_decode_batch_eliminate / _apply).
+  config5 (BASELINE configs[4], strong scaling): ONE fixed job of 4,096 objects × k=128 × 64 KiB split over the
+    N ranks; per object 128 coded pieces encoded and all 128 decoded; a step is the whole job (each rank's share
+    in launches of ≤ 512 objects, pipelined like config2).
 `value` = GiB/s in the reference's own byte counters (SURVEY.md §6 / BASELINE.md): per object
-64 × (k·L + k + L) for the 64 coded pieces (benches/full_rlnc_encoder.rs:111-113) + k·(k+L) for the decode
+n × (k·L + k + L) for the n coded pieces (benches/full_rlnc_encoder.rs:111-113) + k·(k+L) for the decode
 (benches/full_rlnc_decoder.rs:118), summed over all ranks, ÷ the max-over-ranks wall time of the timed steps.
-Multi-GPU: objects are sharded across ranks (weak scaling), no data-path collective; the only collectives
-are the timing barrier and the max/sum reductions of the result.
+Those counters charge the source k·L once per coded piece although one pass serves all n, so `value` is not
+bytes moved: `breakdown.roundtrip_goodput_GiBps` (source bytes through encode + decode) sits beside it, and the
+roofline is the kernel's own: GF(2^8) multiply-adds/s against the measured XOR3-issue ceiling (measure/).
+Multi-GPU: objects are sharded across ranks, no data-path collective; the only collectives are the timing barrier
+and the max/sum reductions of the result.  `--gpus N` without a launcher (WORLD_SIZE unset) starts N rank
+processes itself (fresh interpreters, before any GPU call) with the same arguments.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import platform
+import socket
 import subprocess
 import sys
 import time
@@ -31,6 +41,13 @@ sys.path.insert(0, ROOT)
 METRIC = "device-resident RLNC encode+decode GiB/s, k=32 × 1 MiB, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GIB = float(1 << 30)
+MA_PER_XOR3 = 256  # GF(2^8) multiply-adds per v_bitop3 XOR3 of the bit-sliced kernel (measure/gf_ceiling.hip)
+
+WORKLOADS = {
+    # name: k, L, coded n, decoded-from m, objects (per rank for config2, whole job for config5), chunk
+    "config2": dict(k=32, L=1 << 20, n=64, m=32, objects=32, chunk=32, scaling="weak"),
+    "config5": dict(k=128, L=1 << 16, n=128, m=128, objects=4096, chunk=512, scaling="strong"),
+}
 
 
 def encode_counter(k: int, L: int) -> int:
@@ -124,6 +141,39 @@ def timed_loop(step, steps: int, warmup: int, dist: Dist, sync) -> float:
     return dist.allreduce(elapsed, "max")
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """`--gpus N` with no launcher: N fresh rank processes of this script (same arguments), one per GPU,
+    rendezvous on 127.0.0.1.  This process never touches the GPU.  Returns the first nonzero exit code (the
+    other ranks are stopped then, so a failed rank cannot leave the rest waiting in a barrier)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code and not rc:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 # ------------------------------------------------------------------------------------------------------
 # CPU baseline: the oracle (C restatement of the reference's algorithm) — "port"
 # ------------------------------------------------------------------------------------------------------
@@ -173,8 +223,10 @@ def cpu_baseline(k: int, L: int, n: int, m: int, seconds: float, threads: int = 
     from oracle.oracle import Oracle
 
     res = [None] * threads
+
     def work(t):
         res[t] = _cpu_object_loop(k, L, n, m, seconds, 0x524C4E43 + t)
+
     ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
     t0 = time.perf_counter()
     for th in ths:
@@ -197,48 +249,150 @@ def cpu_baseline(k: int, L: int, n: int, m: int, seconds: float, threads: int = 
 
 
 # ------------------------------------------------------------------------------------------------------
+# the GF(2^8) multiply-add ceiling, measured live (measure/gf_ceiling.hip)
+# ------------------------------------------------------------------------------------------------------
+def xor3_ceiling() -> dict | None:
+    """Chip-wide v_bitop3 XOR3 issue rate (best of 2 and 4 waves per SIMD, random operands) × 256 multiply-adds
+    per XOR3: the peak of the bit-sliced design.  None if the microbenchmark is not built."""
+    path = os.path.join(ROOT, "measure", "libgf_ceiling.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.gf_xor3_issue_rate.restype = ctypes.c_double
+    lib.gf_xor3_issue_rate.argtypes = [ctypes.c_int, ctypes.c_int]
+    rates = {w: lib.gf_xor3_issue_rate(w, 200000) for w in (2, 4)}
+    if min(rates.values()) <= 0:
+        return None
+    best = max(rates.values())
+    return {"xor3_per_s": {str(w): round(r / 1e12, 4) for w, r in rates.items()},
+            "xor3_unit": "T wave64 instructions/s (whole device)",
+            "peak_T_ma_per_s": round(best * MA_PER_XOR3 / 1e12, 2),
+            "how": "measure/gf_ceiling.hip: only independent v_bitop3_b32 XOR3s, 4 VGPR banks, random operands, "
+                   "2 and 4 waves per SIMD on every CU, HIP events around a ~30 ms launch; × 256 GF(2^8) "
+                   "multiply-adds per XOR3 (8 XOR3s add c·x into the 8 bit-planes of 64 lanes × 32 bytes)"}
+
+
+# ------------------------------------------------------------------------------------------------------
 # GPU run
 # ------------------------------------------------------------------------------------------------------
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--objects", type=int, default=32, help="objects per GPU per step (32: profiles/r01_launch_size.txt)")
-    ap.add_argument("--k", type=int, default=32)
-    ap.add_argument("--piece-bytes", type=int, default=1 << 20)
-    ap.add_argument("--coded", type=int, default=64)
-    ap.add_argument("--decode-from", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 30 for config2, 5 for config5)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 5 for config2, 2 for config5)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS) + ["oracle-cpu"], default="config2",
+                    help="config2: the metric's shape, objects per GPU (weak scaling); config5: BASELINE configs[4], "
+                         "4,096 objects split over the ranks (strong scaling); oracle-cpu: the harness alone with "
+                         "the C oracle as each rank's work and gloo (tests)")
+    ap.add_argument("--objects", type=int, default=None,
+                    help="config2: objects per GPU per step (32: profiles/r01_launch_size.txt); config5: the whole job")
+    ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--piece-bytes", type=int, default=None)
+    ap.add_argument("--coded", type=int, default=None)
+    ap.add_argument("--decode-from", type=int, default=None)
+    ap.add_argument("--chunk", type=int, default=None, help="objects per launch (config5: 512)")
     ap.add_argument("--variant", type=int, default=8, help="matmul kernel variant: 8 as 7 with 64-row tiles of 8 waves above 32 output rows and a barrier every third row (default), 7 bit-sliced, one code block per coefficient, combinations shared through LDS, 6 the same without sharing, 5 bit-sliced relative XOR, 0 perm, 1 nibble-LDS, 2 perm3, 3/4 wide")
     ap.add_argument("--tile-rows", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the live XOR3-issue ceiling microbenchmark")
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="threads of the all-cores CPU baseline (one object each; the box's share is 16 cores per GPU)")
     ap.add_argument("--encode-only", action="store_true", help="diagnostic: time only the encode launch")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="1: the decoder's elimination (reads only the coded pieces' coefficient headers, written "
                          "first) runs on a second stream while the encode's data work runs; 2: as 1, and successive "
-                         "steps overlap (two buffer sets: step i+1's encode runs beside step i's decode); 0: serial")
+                         "launches overlap (two buffer sets: launch i+1's encode runs beside launch i's decode); 0: serial")
     ap.add_argument("--breakdown-steps", type=int, default=24,
-                    help="--pipeline 2: steps of the pipeline-1 form run before the timed loop for the per-part times")
+                    help="--pipeline 2: launches of the pipeline-1 form run before the timed loop for the per-part times")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay each step as one captured HIP graph (the kernels of a step, launched together)")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    if args.workload in WORKLOADS:
+        w = WORKLOADS[args.workload]
+        for name, key in [("k", "k"), ("piece_bytes", "L"), ("coded", "n"), ("decode_from", "m"),
+                          ("objects", "objects"), ("chunk", "chunk")]:
+            if getattr(args, name) is None:
+                setattr(args, name, w[key])
+    big = args.workload == "config5"
+    if args.steps is None:
+        args.steps = 5 if big else 30
+    if args.warmup is None:
+        args.warmup = 2 if big else 5
+    return args
 
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    dist = Dist()
+    if os.environ.get("RLNC_BENCH_FAIL_RANK") == str(dist.rank):  # test hook: a rank dying before rendezvous
+        sys.exit(5)
+    assert dist.world == args.gpus or (dist.world == 1 and args.gpus == 1), \
+        f"--gpus {args.gpus} but WORLD_SIZE={dist.world}"
+    if args.workload == "oracle-cpu":
+        return run_oracle_cpu(args, dist)
+    return run_gpu(args, dist)
+
+
+def run_oracle_cpu(args, dist: Dist):
+    """The harness alone (spawn, rendezvous, barrier-bracketed steps, max-over-ranks time, summed bytes, one JSON
+    line from rank 0) with the C oracle as each rank's work, over gloo: tests/test_distributed.py."""
+    import numpy as np
+
+    from oracle.oracle import Oracle, OracleDecoder
+
+    dist.init("gloo")
+    orc = Oracle()
+    k, L, n, m, B = 8, 512, 12, 8, 3
+    rng = np.random.default_rng(100 + dist.rank)  # each rank owns different objects
+    src = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    co = rng.integers(0, 256, (B, n, k), dtype=np.uint8)
+    last = []
+
+    def step():
+        out = []
+        for o in range(B):
+            coded = orc.encode(src[o], co[o])
+            dec = OracleDecoder(L, k)
+            for p in coded[:m]:
+                dec.decode(p)
+            out.append(dec.padded_payload())
+        last[:] = out
+
+    elapsed = timed_loop(step, args.steps, args.warmup, dist, lambda: None)
+    total = dist.allreduce(float(step_bytes(B, k, L, n) * args.steps), "sum")
+    ok = dist.allreduce(float(all(np.array_equal(last[o], src[o]) for o in range(B))), "sum") == dist.world
+    if dist.rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(total / elapsed / GIB, 6), "unit": "GiB/s",
+                          "n_gpus": dist.world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
+                          "scaling": "weak", "elapsed_s": elapsed, "total_bytes": total, "verified": bool(ok),
+                          "config": {"workload": "oracle-cpu harness test"}}), flush=True)
+    dist.close()
+    if not ok:
+        sys.exit(3)
+
+
+def run_gpu(args, dist: Dist):
     import numpy as np
     import torch
 
-    dist = Dist()
-    assert dist.world == args.gpus or (dist.world == 1 and args.gpus == 1), \
-        f"--gpus {args.gpus} but WORLD_SIZE={dist.world} (launch with torch.distributed.run for N>1)"
     torch.cuda.set_device(dist.local_rank)
     dist.init("nccl")
 
     import rlnc_amd
     from rlnc_amd import batch
 
-    k, L, n, m, B = args.k, args.piece_bytes, args.coded, args.decode_from, args.objects
+    wl = WORKLOADS[args.workload]
+    k, L, n, m = args.k, args.piece_bytes, args.coded, args.decode_from
+    if wl["scaling"] == "weak":
+        objs = args.objects  # per rank
+    else:  # a fixed job split over the ranks (the last ranks take one fewer when it does not divide)
+        objs = args.objects // dist.world + (1 if dist.rank < args.objects % dist.world else 0)
+    C = min(args.chunk, objs)  # objects per launch
+    chunks = [(c0, min(objs, c0 + C)) for c0 in range(0, objs, C)]
     ctx = rlnc_amd.Context(dist.local_rank)
     ctx.set_kernel_variant(args.variant, args.tile_rows)
     dev = torch.device("cuda", dist.local_rank)
@@ -247,73 +401,77 @@ def main():
     # rng.fill_bytes in the reference) and uploaded before timing
     gen = torch.Generator(device=dev)
     gen.manual_seed(0x524C4E43 + dist.rank)
-    src = torch.randint(0, 256, (B, k, L), dtype=torch.uint8, device=dev, generator=gen)
-    coeffs = torch.from_numpy(np.random.default_rng(1000 + dist.rank).integers(0, 256, (B, n, k), dtype=np.uint8)).to(dev)
-    pieces = torch.empty((B, n, k + L), dtype=torch.uint8, device=dev)
-    decoded = torch.empty((B, k, L), dtype=torch.uint8, device=dev)
-    received = pieces[:, :m]
-    piece_status = torch.empty((B, m), dtype=torch.int32, device=dev)
-    object_status = torch.empty(B, dtype=torch.int32, device=dev)
-    data_len = torch.empty(B, dtype=torch.int64, device=dev)
+    src = torch.randint(0, 256, (objs, k, L), dtype=torch.uint8, device=dev, generator=gen)
+    coeffs = torch.from_numpy(np.random.default_rng(1000 + dist.rank).integers(0, 256, (objs, n, k),
+                                                                                 dtype=np.uint8)).to(dev)
 
-    enc_events = []
-    dec_events = []
-    # pipelined step: the coded pieces' headers are written first (one strided copy), then the decoder's
-    # elimination — which reads nothing else — runs on a side stream (its own context) concurrently with the
-    # encode's data work; the data side of the decode waits for both.  Same kernels, same bytes as serial.
+    def buffers(B):
+        return dict(pieces=torch.empty((B, n, k + L), dtype=torch.uint8, device=dev),
+                    decoded=torch.empty((B, k, L), dtype=torch.uint8, device=dev),
+                    pst=torch.empty((B, m), dtype=torch.int32, device=dev),
+                    ost=torch.empty(B, dtype=torch.int32, device=dev),
+                    dl=torch.empty(B, dtype=torch.int64, device=dev),
+                    T=torch.empty((B, k, m), dtype=torch.uint8, device=dev),
+                    rank=torch.empty(B, dtype=torch.int32, device=dev),
+                    obj=(0, 0))
+
+    sets = [buffers(C)]
+    enc_events, dec_events = [], []
     ctx_side = rlnc_amd.Context(dist.local_rank) if args.pipeline else None
     side = torch.cuda.Stream(dev) if args.pipeline else None
     ev_start, ev_elim = torch.cuda.Event(), torch.cuda.Event()
-    T = torch.empty((B, k, m), dtype=torch.uint8, device=dev)
-    rank = torch.empty(B, dtype=torch.int32, device=dev)
 
-    def encode_launches():
+    def views(S, c0, c1):
+        b = c1 - c0
+        return (src[c0:c1], coeffs[c0:c1], S["pieces"][:b], S["decoded"][:b], S["pst"][:b], S["ost"][:b],
+                S["dl"][:b], S["T"][:b], S["rank"][:b])
+
+    # one launch group = one chunk of objects: encode then decode, HIP events on the launch stream bracket each
+    # part (pipelined: the encode part includes the concurrent elimination's interference, the decode part any
+    # wait for it)
+    def launch_serial(c0, c1, S):
+        s_, co, pieces, decoded, pst, ost, dl, T, rank = views(S, c0, c1)
+        received = pieces[:, :m]
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
         if args.pipeline:
-            # side stream: the coded pieces' headers (bytes 0..k of each piece), then the elimination over them;
-            # launch stream: the data bytes k.. of the same pieces (disjoint bytes), concurrently
+            # side stream: the coded pieces' headers (bytes 0..k of each piece), then the elimination over
+            # them; launch stream: the data bytes k.. of the same pieces (disjoint bytes), concurrently
             ev_start.record()
             with torch.cuda.stream(side):
                 side.wait_event(ev_start)
-                batch.encode_batch_headers(coeffs, pieces, ctx_side)
+                batch.encode_batch_headers(co, pieces, ctx_side)
                 if not args.encode_only:
-                    batch.decode_batch_eliminate(received, k, T, piece_status, rank, ctx_side)
+                    batch.decode_batch_eliminate(received, k, T, pst, rank, ctx_side)
                 ev_elim.record()
-            batch.encode_batch_data(src, coeffs, pieces, ctx)
+            batch.encode_batch_data(s_, co, pieces, ctx)
             if args.encode_only:
                 torch.cuda.current_stream().wait_event(ev_elim)
         else:
-            batch.encode_batch(src, coeffs, pieces, ctx)
-
-    def decode_launches():
-        if args.encode_only:
-            return
-        if args.pipeline:
-            torch.cuda.current_stream().wait_event(ev_elim)
-            batch.decode_batch_apply(received, k, T, rank, decoded, object_status, data_len, ctx)
-        else:
-            batch.decode_batch_device(received, k, decoded, piece_status, object_status, data_len, ctx)
-
-    def step():
-        # encode, then the device-side decode (elimination + T×data + marker scan), asynchronous; HIP events
-        # on the launch stream bracket each part (pipelined: the encode part includes the concurrent elimination's
-        # interference, the decode part any wait for it)
-        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-        e0.record()
-        encode_launches()
+            batch.encode_batch(s_, co, pieces, ctx)
         e1.record()
-        decode_launches()
+        if not args.encode_only:
+            if args.pipeline:
+                torch.cuda.current_stream().wait_event(ev_elim)
+                batch.decode_batch_apply(received, k, T, rank, decoded, ost, dl, ctx)
+            else:
+                batch.decode_batch_device(received, k, decoded, pst, ost, dl, ctx)
         e2.record()
+        S["obj"] = (c0, c1)
         enc_events.append((e0, e1))
         dec_events.append((e1, e2))
 
-    # --pipeline 2: step i uses buffer set i % 2; its headers + elimination (side stream), encode data (launch
-    # stream) and decode data side (decode stream) wait only for step i-2's decode to release that set, so step
-    # i+1's encode fills the GPU beside step i's decode (no tail or launch gaps between the big kernels)
-    if args.pipeline == 2 and not args.encode_only:
-        sets = [dict(pieces=pieces, decoded=decoded, pst=piece_status, ost=object_status, dl=data_len, T=T, rank=rank)]
-        sets.append(dict(pieces=torch.empty_like(pieces), decoded=torch.empty_like(decoded),
-                         pst=torch.empty_like(piece_status), ost=torch.empty_like(object_status),
-                         dl=torch.empty_like(data_len), T=torch.empty_like(T), rank=torch.empty_like(rank)))
+    def step_serial():
+        for c0, c1 in chunks:
+            launch_serial(c0, c1, sets[0])
+
+    # --pipeline 2: launch group i uses buffer set i % 2; its headers + elimination (side stream), encode data
+    # (launch stream) and decode data side (decode stream) wait only for group i-2's decode to release that
+    # set, so group i+1's encode fills the GPU beside group i's decode (no tail or launch gaps between the big
+    # kernels).  Every group still does all of its work.
+    pipelined = args.pipeline == 2 and not args.encode_only
+    if pipelined:
+        sets.append(buffers(C))
         ctx_dec = rlnc_amd.Context(dist.local_rank)
         ctx_dec.set_kernel_variant(args.variant, args.tile_rows)
         s_dec = torch.cuda.Stream(dev)
@@ -322,128 +480,149 @@ def main():
         ev_el = [torch.cuda.Event(), torch.cuda.Event()]
         count = [0]
 
-        def step2():
+        def launch_pipelined(c0, c1):
             i = count[0]
             count[0] += 1
             bi = i % 2
             S = sets[bi]
-            rec = S["pieces"][:, :m]
+            s_, co, pieces, decoded, pst, ost, dl, T, rank = views(S, c0, c1)
+            rec = pieces[:, :m]
             with torch.cuda.stream(side):
                 if i >= 2:
                     side.wait_event(ev_done[bi])
-                batch.encode_batch_headers(coeffs, S["pieces"], ctx_side)
-                batch.decode_batch_eliminate(rec, k, S["T"], S["pst"], S["rank"], ctx_side)
+                batch.encode_batch_headers(co, pieces, ctx_side)
+                batch.decode_batch_eliminate(rec, k, T, pst, rank, ctx_side)
                 ev_el[bi].record()
             if i >= 2:
                 torch.cuda.current_stream().wait_event(ev_done[bi])
-            batch.encode_batch_data(src, coeffs, S["pieces"], ctx)
+            batch.encode_batch_data(s_, co, pieces, ctx)
             ev_enc[bi].record()
             with torch.cuda.stream(s_dec):
                 s_dec.wait_event(ev_enc[bi])
                 s_dec.wait_event(ev_el[bi])
-                batch.decode_batch_apply(rec, k, S["T"], S["rank"], S["decoded"], S["ost"], S["dl"], ctx_dec)
+                batch.decode_batch_apply(rec, k, T, rank, decoded, ost, dl, ctx_dec)
                 ev_done[bi].record()
+            S["obj"] = (c0, c1)
 
-    run = step2 if args.pipeline == 2 and not args.encode_only else step
+        def step_pipelined():
+            for c0, c1 in chunks:
+                launch_pipelined(c0, c1)
+
+    run = step_pipelined if pipelined else step_serial
+    skip = args.warmup * len(chunks)
     if args.graph:
         # eager warmup steps (they also give the per-kernel breakdown), then capture one step's launches into
         # a graph: the timed steps replay it, identical kernels and work, without per-launch host overhead
         for _ in range(max(args.warmup, 2)):
-            step()
+            step_serial()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            encode_launches()
-            decode_launches()
+            step_serial()
         run = g.replay
-    if run is not step and not args.graph:
-        # --pipeline 2: the per-part times (encode launch for the roofline, decode) come from pipeline-1 steps run
-        # before the timed loop (the first 6 discarded: clocks and caches settle): a kernel's own duration, not its
-        # overlap with the next step's kernels
-        for _ in range(args.breakdown_steps + 6):
-            step()
+    elif pipelined:
+        # the per-part times (encode launch for the roofline, decode) come from pipeline-1 launch groups run
+        # before the timed loop (the first 6 discarded: clocks and caches settle): a kernel's own duration, not
+        # its overlap with the next group's kernels
+        for i in range(args.breakdown_steps + 6):
+            c0, c1 = chunks[i % len(chunks)]
+            launch_serial(c0, c1, sets[0])
         torch.cuda.synchronize()
+        skip = 6
     elapsed = timed_loop(run, args.steps, args.warmup, dist, torch.cuda.synchronize)
     torch.cuda.synchronize()
-    skip = 0 if args.graph else args.warmup  # graph mode: the eager warmup steps carry the breakdown
-    def verified(vdec, vpst, vost):
-        # every full-rank object decodes to its source
-        pst, ost = vpst.cpu().numpy(), vost.cpu().numpy()
+
+    def verified(S):
+        # every full-rank object of the last launch group that used this set decodes to its source
+        c0, c1 = S["obj"]
+        b = c1 - c0
+        pst, ost = S["pst"][:b].cpu().numpy(), S["ost"][:b].cpu().numpy()
         good = True
-        for o in range(B):
+        for o in range(b):
             if (pst[o] == 0).sum() == k:
-                good = good and torch.equal(vdec[o], src[o])
+                good = good and torch.equal(S["decoded"][o], src[c0 + o])
             else:
                 good = good and int(ost[o]) == 10  # NotAllPiecesReceivedYet (rank-deficient draw)
         return good and bool((pst == 0).sum(axis=1).max() == k)
 
-    # correctness of what was timed: the last step's outputs (--pipeline 2: the last two steps', one per buffer set)
     ok = True
-    if run is not step and not args.graph:  # --pipeline 2
+    if not args.encode_only:
         for S in sets:
-            ok = ok and verified(S["decoded"], S["pst"], S["ost"])
-        skip = 6
-    elif not args.encode_only:
-        ok = verified(decoded, piece_status, object_status)
-    timed_enc = enc_events[skip:]
+            ok = ok and verified(S)
+    ok = dist.allreduce(float(ok), "sum") == dist.world
+    timed_enc = enc_events[skip:] or enc_events
     enc_ms = sum(a.elapsed_time(b) for a, b in timed_enc) / len(timed_enc)
-    timed_dec = dec_events[skip:]
+    timed_dec = dec_events[skip:] or dec_events
     dec_ms = sum(a.elapsed_time(b) for a, b in timed_dec) / len(timed_dec)
 
-    per_rank_bytes = step_bytes(B, k, L, n) if not args.encode_only else B * n * encode_counter(k, L)
+    per_rank_bytes = step_bytes(objs, k, L, n) if not args.encode_only else objs * n * encode_counter(k, L)
     total_bytes = dist.allreduce(float(per_rank_bytes * args.steps), "sum")
+    total_objs = dist.allreduce(float(objs), "sum")
     value = total_bytes / elapsed / GIB
 
-    # roofline of the dominant kernel (the encode matmul, one launch per step) from HIP events
-    enc_alg = B * n * encode_counter(k, L)           # reference counter bytes per launch
+    # roofline of the dominant kernel (the encode matmul, one launch per launch group) from HIP events.  The
+    # kernel is bound by VALU issue, not HBM: `achieved` = its GF(2^8) multiply-adds per second,
+    # `peak` = the live XOR3-issue ceiling of the bit-sliced design; the HBM view (compulsory bytes: source once
+    # + coded pieces written, and the PMC-measured traffic) sits beside it.
+    B = C
+    ma_per_launch = B * n * k * L                    # GF(2^8) multiply-adds per encode launch
+    achieved = ma_per_launch / (enc_ms * 1e-3) / 1e12
+    enc_alg = B * n * encode_counter(k, L)           # reference-counter bytes per launch
     enc_compulsory = B * (k * L + n * (k + L))       # source read once + coded pieces written
-    achieved = enc_alg / (enc_ms * 1e-3) / 1e9
-    ma_per_launch = B * n * k * L                    # GF(2^8) multiply-adds per launch
     variant = VARIANTS[args.variant]
     traffic, traffic_src = pmc_traffic(variant, B, k, L, n)
+    ceiling = None if args.no_ceiling else xor3_ceiling()
+    peak = ceiling["peak_T_ma_per_s"] if ceiling else None
     roofline = {
-        "bound": "hbm",
-        "achieved": round(achieved, 1),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "bound": "valu",
+        "achieved": round(achieved, 2),
+        "peak": peak,
+        "unit": "T GF(2^8) multiply-adds/s",
+        "frac": round(achieved / peak, 4) if peak else None,
         "traffic": traffic,
         "traffic_source": traffic_src,
         "kernel": f"{KERNELS[variant]} (encode: {n} coded pieces x {B} objects per launch)",
         "kernel_ms": round(enc_ms, 4),
-        "kernel_ms_how": ("HIP events around the encode launch on its stream, in pipeline-1 steps (the elimination "
-                          "beside it, no other step's kernels)") if args.pipeline else "HIP events around the encode launch",
-        "outputs_per_pass": n,
-        "compulsory_bytes": enc_compulsory,
-        "compulsory_GBps": round(enc_compulsory / (enc_ms * 1e-3) / 1e9, 1),
-        "compulsory_frac": round(enc_compulsory / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-        "gf_muladd_per_s": round(ma_per_launch / (enc_ms * 1e-3) / 1e12, 3),
-        "gf_muladd_unit": "T byte-multiply-adds/s",
+        "kernel_ms_how": ("HIP events around the encode launch on its stream, in pipeline-1 launch groups (the "
+                          "elimination beside it, no other group's kernels)") if args.pipeline else
+                         "HIP events around the encode launch",
+        "multiply_adds_per_launch": ma_per_launch,
+        "ceiling": ceiling,
+        "hbm": {"compulsory_bytes": enc_compulsory,
+                "compulsory_GBps": round(enc_compulsory / (enc_ms * 1e-3) / 1e9, 1),
+                "peak_GBps": HBM_PEAK_GBS,
+                "compulsory_frac": round(enc_compulsory / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "traffic_over_compulsory": round(traffic / enc_compulsory, 4) if traffic else None},
+        "refcounter": {"bytes_per_launch": enc_alg, "GBps": round(enc_alg / (enc_ms * 1e-3) / 1e9, 1),
+                       "note": "the reference's encoder byte counter charges the source once per coded piece; "
+                               f"{n} coded pieces share one source pass, so this is not a bandwidth"},
     }
 
     # supplementary HBM roofline: the same source, ONE coded piece per object per launch (configs[1]'s encode
     # at one output row, ~1 multiply-add per source byte: the HBM-bound form of the north star's "encode at
     # k=32 x 1 MiB"); not part of `value`
     single = None
-    if not args.encode_only:
-        co1 = coeffs[:, :1].contiguous()
-        out1 = torch.empty((B, 1, k + L), dtype=torch.uint8, device=dev)
+    if not args.encode_only and args.workload == "config2":
+        c0, c1 = chunks[0]
+        co1 = coeffs[c0:c1, :1].contiguous()
+        out1 = torch.empty((c1 - c0, 1, k + L), dtype=torch.uint8, device=dev)
         ts = []
         for r in range(12):
             a, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            batch.encode_batch(src, co1, out1, ctx)
+            batch.encode_batch(src[c0:c1], co1, out1, ctx)
             b_.record()
             torch.cuda.synchronize()
             if r >= 2:
                 ts.append(a.elapsed_time(b_))
         ms1 = sorted(ts)[len(ts) // 2]
-        ok1 = torch.equal(out1[:, 0, k:], pieces[:, 0, k:])  # = coded piece 0 of the timed encode
-        read1 = B * (k * L + k)
+        S0 = sets[0]  # holds the timed encode of chunk 0 (config2 has one launch group per step)
+        ok1 = S0["obj"] == (c0, c1) and torch.equal(out1[:, 0, k:], S0["pieces"][: c1 - c0, 0, k:])
+        read1 = (c1 - c0) * (k * L + k)
         single = {"coded_per_pass": 1, "kernel": "gf_matmul_stream_kernel<1, 2>", "ms": round(ms1, 4),
                   "source_read_GBps": round(read1 / ms1 / 1e6, 1),
                   "read_frac": round(read1 / ms1 / 1e6 / HBM_PEAK_GBS, 4),
-                  "compulsory_GBps": round((read1 + B * (k + L)) / ms1 / 1e6, 1), "verified": bool(ok1)}
+                  "compulsory_GBps": round((read1 + (c1 - c0) * (k + L)) / ms1 / 1e6, 1), "verified": bool(ok1)}
 
     result = {
         "metric": METRIC,
@@ -454,20 +633,24 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": wl["scaling"],
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: uniform random source bytes (torch generator, seeded per rank), coefficients "
                 "uniform bytes from a seeded host RNG",
         "config": {
-            "workload": f"per object: encode k={k} x {L} B -> {n} coded pieces (configs[1]) + decode from the "
-                        f"first {m} (configs[2]); {B} objects per GPU per step",
-            "k": k, "piece_bytes": L, "coded_per_object": n, "decoded_from": m, "objects_per_gpu": B,
+            "workload": (f"configs[1]+[2]: per object encode k={k} x {L} B -> {n} coded pieces + decode from the "
+                         f"first {m}; {objs} objects per GPU per step") if args.workload == "config2" else
+                        (f"configs[4]: {int(total_objs)} objects x k={k} x {L} B split over {dist.world} rank(s) "
+                         f"({objs} on rank {dist.rank}), encode {n} coded + decode {m} per object, "
+                         f"launches of {C} objects; one step = the whole job"),
+            "k": k, "piece_bytes": L, "coded_per_object": n, "decoded_from": m, "objects_per_gpu": objs,
+            "objects_total": int(total_objs), "objects_per_launch": C,
             "parallelism": f"objects sharded over {dist.world} rank(s), no data-path collective",
             "kernel_variant": variant,
             "pipeline": {0: "serial", 1: "elimination on a side stream concurrent with the encode data work",
-                         2: "elimination beside the encode data work, and step i+1's encode beside step i's decode "
-                            "(two buffer sets)"}[args.pipeline],
+                         2: "elimination beside the encode data work, and launch group i+1's encode beside group "
+                            "i's decode (two buffer sets)"}[args.pipeline],
         },
         "roofline": roofline,
         "hbm_single_pass_encode": single,
@@ -475,9 +658,11 @@ def main():
         "breakdown": {
             "encode_kernel_ms": round(enc_ms, 4),
             "decode_ms": round(dec_ms, 4),
+            "encode_T_ma_per_s": round(achieved, 2),
             "encode_GiBps_refcounter": round(B * n * encode_counter(k, L) / (enc_ms * 1e-3) / GIB, 1),
             "decode_GiBps_refcounter": round(B * decode_counter(k, L) / (dec_ms * 1e-3) / GIB, 2) if dec_ms else None,
-            "roundtrip_goodput_GiBps": round(dist.world * B * k * L * args.steps / elapsed / GIB, 2),
+            "roundtrip_goodput_GiBps": round(total_objs * k * L * args.steps / elapsed / GIB, 2),
+            "roundtrip_goodput_note": "source bytes encoded and decoded per second, all ranks (not reference counters)",
             "verified": ok,
         },
     }

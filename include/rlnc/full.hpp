@@ -86,7 +86,8 @@ inline Result<void> status(int s) {
     throw DeviceError(std::string(rlnc_status_name(s)) + ": " + rlnc_last_error());
 }
 
-// one context per host thread (the reference's &mut self types are single-threaded per object)
+// The default context of the calling thread.  Objects take their own reference on it (rlnc_hip.h, Lifetime), so
+// an Encoder built on a worker thread stays valid after that thread -- and this thread_local -- is gone.
 inline rlnc_context *context() {
     thread_local struct Holder {
         rlnc_context *c = nullptr;
@@ -114,6 +115,16 @@ struct Handle {
         if (h) Free(h);
     }
 };
+
+// #[derive(Clone)] of the reference types: an independent librlnc_hip object
+template <class H>
+H *clone_handle(int (*fn)(const H *, H **), const H *h) {
+    if (!h) return nullptr;
+    H *c = nullptr;
+    const int s = fn(h, &c);
+    if (s != RLNC_OK) throw DeviceError(std::string("clone: ") + rlnc_last_error());
+    return c;
+}
 }  // namespace detail
 
 namespace full {
@@ -122,6 +133,15 @@ namespace full {
 class Encoder {
    public:
     Encoder() = default;
+    Encoder(const Encoder &o) : h_(detail::clone_handle(rlnc_encoder_clone, o.h_.h)) {}  // Clone
+    Encoder &operator=(const Encoder &o) {
+        Encoder t(o);
+        std::swap(h_.h, t.h_.h);
+        return *this;
+    }
+    Encoder(Encoder &&) noexcept = default;
+    Encoder &operator=(Encoder &&) noexcept = default;
+    Encoder clone() const { return Encoder(*this); }
     static Result<Encoder> create(const std::vector<uint8_t> &data, size_t piece_count) {  // Encoder::new :85
         rlnc_encoder *h = nullptr;
         auto r = detail::status(rlnc_encoder_new(detail::context(), data.data(), data.size(), piece_count, &h));
@@ -154,6 +174,15 @@ class Encoder {
 class Decoder {
    public:
     Decoder() = default;
+    Decoder(const Decoder &o) : h_(detail::clone_handle(rlnc_decoder_clone, o.h_.h)) {}  // Clone
+    Decoder &operator=(const Decoder &o) {
+        Decoder t(o);
+        std::swap(h_.h, t.h_.h);
+        return *this;
+    }
+    Decoder(Decoder &&) noexcept = default;
+    Decoder &operator=(Decoder &&) noexcept = default;
+    Decoder clone() const { return Decoder(*this); }
     static Result<Decoder> create(size_t piece_byte_len, size_t required_piece_count) {  // Decoder::new :65
         rlnc_decoder *h = nullptr;
         auto r = detail::status(rlnc_decoder_new(detail::context(), piece_byte_len, required_piece_count, &h));
@@ -188,6 +217,15 @@ class Decoder {
 class Recoder {
    public:
     Recoder() = default;
+    Recoder(const Recoder &o) : h_(detail::clone_handle(rlnc_recoder_clone, o.h_.h)) {}  // Clone
+    Recoder &operator=(const Recoder &o) {
+        Recoder t(o);
+        std::swap(h_.h, t.h_.h);
+        return *this;
+    }
+    Recoder(Recoder &&) noexcept = default;
+    Recoder &operator=(Recoder &&) noexcept = default;
+    Recoder clone() const { return Recoder(*this); }
     static Result<Recoder> create(const std::vector<uint8_t> &data, size_t full_coded_piece_byte_len,
                                   size_t num_pieces_coded_together) {  // Recoder::new :68
         rlnc_recoder *h = nullptr;

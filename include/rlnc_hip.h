@@ -19,8 +19,19 @@
  *   - "_device" / batch functions take device pointers (hipMalloc'd memory on the context's device) and
  *     are asynchronous on the context's stream; the object API (encoder/decoder/recoder on host buffers)
  *     is synchronous, like the Rust API it mirrors.
- *   - One context per host thread (mirrors &mut self of Decoder/Recoder); objects are bound to the
- *     context that created them.
+ *   - Threading.  The object API (Encoder/Decoder/Recoder on host buffers) is safe to call from many host
+ *     threads on one context: every call leases its own stream and buffers from the context's pool, so
+ *     rlnc_encoder_code_with_buf on ONE encoder from many threads at once is safe, like the reference's
+ *     code(&self) on a Send + Sync Encoder (encoder.rs:264).  A decoder or recoder must not be used by two
+ *     threads at the same time (the reference's &mut self).  The stream-ordered batch / _device calls use the
+ *     context's own workspaces: one caller thread per context at a time (one context per stream).
+ *   - Lifetime.  Objects hold a reference on the context that created them: rlnc_context_destroy drops the
+ *     creator's reference and the context is freed when its last object is freed, so an object may outlive
+ *     the thread (and thread-local context) that created it.
+ *   - HIP graphs.  Once a batch call on a context has been captured into a HIP graph, the graph holds that
+ *     context's workspace addresses: they are frozen, and a later call that would need a larger workspace
+ *     fails with RLNC_ERR_INVALID_ARGUMENT instead of moving them (run the largest shape eagerly before
+ *     capturing, or use another context for other shapes).
  */
 #ifndef RLNC_HIP_H
 #define RLNC_HIP_H
@@ -131,6 +142,9 @@ int rlnc_encoder_without_padding(rlnc_context *ctx, const uint8_t *data, size_t 
  * outlive the encoder). */
 int rlnc_encoder_from_device(rlnc_context *ctx, const uint8_t *pieces_dev, size_t piece_count, size_t piece_len,
                              size_t row_stride, rlnc_encoder **out);
+/* #[derive(Clone)] (encoder.rs:18): an independent copy (an owned source is copied on the device; a borrowed
+ * device source stays borrowed). */
+int rlnc_encoder_clone(const rlnc_encoder *enc, rlnc_encoder **out);
 void rlnc_encoder_free(rlnc_encoder *enc);
 size_t rlnc_encoder_get_piece_count(const rlnc_encoder *enc);              /* encoder.rs:27-29 */
 size_t rlnc_encoder_get_piece_byte_len(const rlnc_encoder *enc);           /* encoder.rs:32-34 */
@@ -153,6 +167,7 @@ typedef struct rlnc_recoder rlnc_recoder;
 /* Recoder::new (recoder.rs:68-108); data = concatenated full coded pieces (host, copied). */
 int rlnc_recoder_new(rlnc_context *ctx, const uint8_t *data, size_t data_len, size_t full_coded_piece_byte_len,
                      size_t num_pieces_coded_together, rlnc_recoder **out);
+int rlnc_recoder_clone(const rlnc_recoder *rec, rlnc_recoder **out); /* #[derive(Clone)], recoder.rs:12 */
 void rlnc_recoder_free(rlnc_recoder *rec);
 size_t rlnc_recoder_get_original_num_pieces_coded_together(const rlnc_recoder *rec); /* recoder.rs:26-28 */
 size_t rlnc_recoder_get_num_pieces_recoded_together(const rlnc_recoder *rec);       /* recoder.rs:31-33 */
@@ -169,6 +184,8 @@ int rlnc_recoder_recode_batch_device(rlnc_recoder *rec, const uint8_t *r_dev, si
 typedef struct rlnc_decoder rlnc_decoder;
 /* Decoder::new(piece_byte_len, required_piece_count) (decoder.rs:65-80; note the argument order). */
 int rlnc_decoder_new(rlnc_context *ctx, size_t piece_byte_len, size_t required_piece_count, rlnc_decoder **out);
+/* #[derive(Clone)] (decoder.rs:8): elimination state, counters and the received data rows are copied. */
+int rlnc_decoder_clone(const rlnc_decoder *dec, rlnc_decoder **out);
 void rlnc_decoder_free(rlnc_decoder *dec);
 /* Decoder::decode (decoder.rs:96-118): Ok / PieceNotUseful / ReceivedAllPieces / InvalidPieceLength.
  * The accept/reject answer is immediate (exact replica of the diagonal-pivot RREF on the coefficient

@@ -51,6 +51,7 @@ _SIGS = {
     "rlnc_encoder_new": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.POINTER(vp)]),
     "rlnc_encoder_without_padding": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.POINTER(vp)]),
     "rlnc_encoder_from_device": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.POINTER(vp)]),
+    "rlnc_encoder_clone": (C.c_int, [vp, C.POINTER(vp)]),
     "rlnc_encoder_free": (None, [vp]),
     "rlnc_encoder_get_piece_count": (C.c_size_t, [vp]),
     "rlnc_encoder_get_piece_byte_len": (C.c_size_t, [vp]),
@@ -59,6 +60,7 @@ _SIGS = {
     "rlnc_encoder_code_with_buf": (C.c_int, [vp, vp, C.c_size_t, vp, C.c_size_t]),
     "rlnc_encoder_code_batch_device": (C.c_int, [vp, vp, C.c_size_t, vp, C.c_size_t]),
     "rlnc_recoder_new": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.POINTER(vp)]),
+    "rlnc_recoder_clone": (C.c_int, [vp, C.POINTER(vp)]),
     "rlnc_recoder_free": (None, [vp]),
     "rlnc_recoder_get_original_num_pieces_coded_together": (C.c_size_t, [vp]),
     "rlnc_recoder_get_num_pieces_recoded_together": (C.c_size_t, [vp]),
@@ -67,6 +69,7 @@ _SIGS = {
     "rlnc_recoder_recode_with_buf": (C.c_int, [vp, vp, C.c_size_t, vp, C.c_size_t]),
     "rlnc_recoder_recode_batch_device": (C.c_int, [vp, vp, C.c_size_t, vp]),
     "rlnc_decoder_new": (C.c_int, [vp, C.c_size_t, C.c_size_t, C.POINTER(vp)]),
+    "rlnc_decoder_clone": (C.c_int, [vp, C.POINTER(vp)]),
     "rlnc_decoder_free": (None, [vp]),
     "rlnc_decoder_decode": (C.c_int, [vp, vp, C.c_size_t]),
     "rlnc_decoder_decode_device": (C.c_int, [vp, vp, C.c_size_t]),

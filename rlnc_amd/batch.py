@@ -14,12 +14,20 @@ import ctypes as C
 import numpy as np
 
 from ._lib import MatmulDesc
-from .context import Context, default_context
+from .context import Context, stream_context
 from .errors import check
 
 
 def _ctx_for(t, ctx: Context | None) -> Context:
-    ctx = ctx or default_context(t.device.index or 0)
+    """The context a batch call launches with, on torch's current stream.  Without an explicit ctx each
+    (device, stream) pair gets its own default context: a context's workspaces are stream-ordered, so two
+    streams sharing one would overwrite each other's in-flight index stream / transform (include/rlnc_hip.h,
+    Threading)."""
+    import torch
+
+    dev = t.device.index or 0
+    if ctx is None:
+        return stream_context(dev, torch.cuda.current_stream(dev).cuda_stream)
     ctx.use_torch_stream()
     return ctx
 

@@ -69,4 +69,17 @@ def default_context(device: int = 0) -> Context:
     return ctxs[device]
 
 
-__all__ = ["Context", "default_context", "RLNCError"]
+def stream_context(device: int, stream_handle: int) -> Context:
+    """This thread's context bound to one HIP stream (created on first use and kept)."""
+    ctxs = getattr(_tls, "sctxs", None)
+    if ctxs is None:
+        ctxs = _tls.sctxs = {}
+    key = (device, int(stream_handle or 0))
+    c = ctxs.get(key)
+    if c is None:
+        c = ctxs[key] = Context(device)
+        c.set_stream(key[1])
+    return c
+
+
+__all__ = ["Context", "default_context", "stream_context", "RLNCError"]

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -98,7 +100,23 @@ struct PinBuf {
 
 }  // namespace
 
+// Workspace of one object-API call (Encoder/Recoder/Decoder on host buffers): its own stream, scratch and
+// staging buffers, leased from the context's pool for the duration of the call.  Concurrent calls on one
+// context (e.g. Encoder::code(&self) from many threads, encoder.rs:264 -- the reference type is Send + Sync)
+// therefore never share a buffer.
+struct CallWs {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev = nullptr;
+    DevBuf coef, out, idx, scan, status, len;
+    PinBuf pin_a, pin_b, pin_c;
+    ~CallWs() {
+        if (ev) (void)hipEventDestroy(ev);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
 struct rlnc_context {
+    std::atomic<int> refs{1};  // the creator's reference + one per Encoder/Decoder/Recoder bound to it
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
@@ -107,14 +125,76 @@ struct rlnc_context {
     int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination,
                           // 3 device elimination with the clean state on LDS, 4 ... on one wave's
                           // registers (A/B)
+    // workspaces of the stream-ordered batch / _device API (one caller thread per context at a time)
     DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len, ws_pstat, ws_rank, ws_idx;
     PinBuf pin_a, pin_b, pin_c;
+    // set once a batch call ran inside a HIP stream capture: the graph holds the workspace addresses, so
+    // they must never move again (grow() refuses instead of reallocating)
+    std::atomic<bool> graph_bound{false};
+    std::mutex pool_mu;
+    std::vector<std::unique_ptr<CallWs>> pool;
 
+    void retain() { refs.fetch_add(1, std::memory_order_relaxed); }
+    void release() {
+        if (refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+        (void)hipSetDevice(device);
+        (void)hipStreamSynchronize(stream);
+        if (own) (void)hipStreamDestroy(own);
+        delete this;  // the buffers' destructors free on this device
+    }
     int activate() const {
         HIP_TRY(hipSetDevice(device));
         return RLNC_OK;
     }
-    int matmul(rlnc::MatmulParams p) {
+    // batch API: note a stream capture in progress (freezes the workspaces)
+    int note_capture() {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_TRY(hipStreamIsCapturing(stream, &cs));
+        if (cs != hipStreamCaptureStatusNone) graph_bound = true;
+        return RLNC_OK;
+    }
+    int grow(DevBuf &b, size_t bytes) {
+        if (bytes <= b.cap) return RLNC_OK;
+        if (graph_bound)
+            return set_error(RLNC_ERR_INVALID_ARGUMENT,
+                             "this context's workspaces are bound to a captured HIP graph and cannot grow to %zu "
+                             "bytes: capture the largest shape first, or use another context",
+                             bytes);
+        return b.ensure(bytes);
+    }
+    int grow(PinBuf &b, size_t bytes) {
+        if (bytes <= b.cap) return RLNC_OK;
+        if (graph_bound)
+            return set_error(RLNC_ERR_INVALID_ARGUMENT,
+                             "this context's workspaces are bound to a captured HIP graph and cannot grow");
+        return b.ensure(bytes);
+    }
+    // a call workspace, ordered after the work already enqueued on the context stream
+    int lease(std::unique_ptr<CallWs> &ws) {
+        {
+            std::lock_guard<std::mutex> lock(pool_mu);
+            if (!pool.empty()) {
+                ws = std::move(pool.back());
+                pool.pop_back();
+            }
+        }
+        if (!ws) {
+            ws.reset(new (std::nothrow) CallWs);
+            if (!ws) return set_error(RLNC_ERR_OUT_OF_MEMORY, "call workspace allocation");
+            HIP_TRY(hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&ws->ev, hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventRecord(ws->ev, stream));
+        HIP_TRY(hipStreamWaitEvent(ws->stream, ws->ev, 0));
+        return RLNC_OK;
+    }
+    void unlease(std::unique_ptr<CallWs> ws) {
+        if (!ws) return;
+        std::lock_guard<std::mutex> lock(pool_mu);
+        pool.push_back(std::move(ws));
+    }
+    // the GF(2^8) matmul on stream s with index scratch idx (batch API: the context's; object API: the lease's)
+    int matmul(rlnc::MatmulParams p, hipStream_t s, DevBuf &idx, bool batch) {
         if (max_tile_rows > 0 && p.n_out > max_tile_rows) {
             // split the output rows into launches of at most max_tile_rows rows (tuning knob)
             const int total = p.n_out;
@@ -124,49 +204,81 @@ struct rlnc_context {
                 q.coef = p.coef + int64_t(r0) * p.coef_row;
                 q.out = p.out + int64_t(r0) * p.out_row;
                 if (p.hdr) q.hdr = p.hdr + int64_t(r0) * p.hdr_row;
-                if (int st = launch(q)) return st;
+                if (int st = launch(q, s, idx, batch)) return st;
             }
             return RLNC_OK;
         }
-        return launch(p);
+        return launch(p, s, idx, batch);
     }
-    int launch(const rlnc::MatmulParams &p) {
-        const size_t need = rlnc::matmul_scratch_bytes(p, variant);
+    int matmul(const rlnc::MatmulParams &p) { return matmul(p, stream, ws_idx, true); }
+    int launch(const rlnc::MatmulParams &p, hipStream_t s, DevBuf &idx, bool batch) {
+        const rlnc::MatmulVariant v = variant;
+        const size_t need = rlnc::matmul_scratch_bytes(p, v);
         if (need)
-            if (int st = ws_idx.ensure(need)) return st;
-        HIP_TRY(rlnc::launch_matmul(p, stream, variant, ws_idx.p, ws_idx.cap));
+            if (int st = batch ? grow(idx, need) : idx.ensure(need)) return st;
+        HIP_TRY(rlnc::launch_matmul(p, s, v, idx.p, idx.cap));
         return RLNC_OK;
     }
 };
 
-struct rlnc_encoder {
+namespace {
+// RAII lease of a call workspace
+struct Lease {
     rlnc_context *ctx;
-    size_t k, L, stride;
+    std::unique_ptr<CallWs> ws;
+    explicit Lease(rlnc_context *c) : ctx(c) {}
+    int acquire() { return ctx->lease(ws); }
+    CallWs *operator->() const { return ws.get(); }
+    ~Lease() { ctx->unlease(std::move(ws)); }
+};
+}  // namespace
+
+// Encoder / Recoder / Decoder hold a reference on their context (released when the object is freed), so an
+// object outlives the handle its creator held -- e.g. one built on a worker thread whose thread-local context
+// has since been destroyed.
+struct rlnc_encoder {
+    rlnc_context *ctx = nullptr;
+    size_t k = 0, L = 0, stride = 0;
     uint8_t *src = nullptr;  // k rows × stride
     bool owned = false;
+    void bind(rlnc_context *c) {
+        ctx = c;
+        c->retain();
+    }
     ~rlnc_encoder() {
         if (owned && src) (void)hipFree(src);
+        if (ctx) ctx->release();
     }
 };
 
 struct rlnc_recoder {
-    rlnc_context *ctx;
-    size_t k, n, full, stride;
+    rlnc_context *ctx = nullptr;
+    size_t k = 0, n = 0, full = 0, stride = 0;
     uint8_t *pieces = nullptr;  // n rows × stride (coeffs ‖ data)
+    void bind(rlnc_context *c) {
+        ctx = c;
+        c->retain();
+    }
     ~rlnc_recoder() {
         if (pieces) (void)hipFree(pieces);
+        if (ctx) ctx->release();
     }
 };
 
 struct rlnc_decoder {
-    rlnc_context *ctx;
-    size_t k, L, stride;
+    rlnc_context *ctx = nullptr;
+    size_t k = 0, L = 0, stride = 0;
     size_t received = 0, useful = 0;
     std::unique_ptr<Elimination> elim;
     uint8_t *store = nullptr;  // slot rows × stride (received data rows still referenced by E)
     size_t store_slots = 0;
+    void bind(rlnc_context *c) {
+        ctx = c;
+        c->retain();
+    }
     ~rlnc_decoder() {
         if (store) (void)hipFree(store);
+        if (ctx) ctx->release();
     }
 };
 
@@ -192,9 +304,9 @@ int matmul_desc_to_params(const rlnc_matmul_desc *d, rlnc::MatmulParams &p) {
     return RLNC_OK;
 }
 
-// One coded piece on the device: out_dev[0:L) = Σ_j cv[j] · src_j  (cv already on the device)
-int encoder_launch(rlnc_encoder *e, const uint8_t *cv_dev, int64_t cv_row, int n, uint8_t *out_dev, int64_t out_row,
-                   uint8_t *hdr_dev, int64_t hdr_row) {
+// n coded pieces of one encoder: out[i][0:L) = Σ_j cv[i][j] · src_j  (cv already on the device)
+rlnc::MatmulParams encoder_params(const rlnc_encoder *e, const uint8_t *cv_dev, int64_t cv_row, int n,
+                                  uint8_t *out_dev, int64_t out_row, uint8_t *hdr_dev, int64_t hdr_row) {
     rlnc::MatmulParams p{};
     p.in = e->src;
     p.in_row = int64_t(e->stride);
@@ -208,7 +320,7 @@ int encoder_launch(rlnc_encoder *e, const uint8_t *cv_dev, int64_t cv_row, int n
     p.n_in = int(e->k);
     p.width = int64_t(e->L);
     p.n_obj = 1;
-    return e->ctx->matmul(p);
+    return p;
 }
 
 }  // namespace
@@ -294,12 +406,9 @@ int rlnc_context_create(int device, rlnc_context **out) {
     return RLNC_OK;
 }
 
+// Drops the creator's reference; the context lives on while objects bound to it exist.
 void rlnc_context_destroy(rlnc_context *ctx) {
-    if (!ctx) return;
-    (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->own) (void)hipStreamDestroy(ctx->own);
-    delete ctx;
+    if (ctx) ctx->release();
 }
 
 int rlnc_context_set_stream(rlnc_context *ctx, void *s) {
@@ -347,7 +456,7 @@ int rlnc_gf256_inplace_mul_vec_by_scalar(rlnc_context *ctx, uint8_t *vec, size_t
     if (len == 0) return RLNC_OK;  // :19-21
     CHECK_ARG(vec != nullptr);
     int st = ctx->activate();
-    if (st) return st;
+    if (st || (st = ctx->note_capture())) return st;
     if (scalar == 0) {  // :22-25
         HIP_TRY(hipMemsetAsync(vec, 0, len, ctx->stream));
         return RLNC_OK;
@@ -362,7 +471,7 @@ int rlnc_gf256_inplace_add_vectors(rlnc_context *ctx, uint8_t *dst, const uint8_
     if (len == 0) return RLNC_OK;
     CHECK_ARG(dst != nullptr && src != nullptr);
     int st = ctx->activate();
-    if (st) return st;
+    if (st || (st = ctx->note_capture())) return st;
     HIP_TRY(rlnc::launch_add_vectors(dst, src, int64_t(len), ctx->stream));
     return RLNC_OK;
 }
@@ -374,7 +483,7 @@ int rlnc_gf256_mul_vec_by_scalar_then_add_into_vec(rlnc_context *ctx, uint8_t *d
     if (scalar == 0) return RLNC_OK;  // :93-95
     CHECK_ARG(dst != nullptr && src != nullptr);
     int st = ctx->activate();
-    if (st) return st;
+    if (st || (st = ctx->note_capture())) return st;
     if (scalar == 1) {  // :96-99
         HIP_TRY(rlnc::launch_add_vectors(dst, src, int64_t(len), ctx->stream));
         return RLNC_OK;
@@ -389,7 +498,7 @@ int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc) {
     if (desc->n_out == 0 || desc->width == 0 || desc->n_obj == 0) return RLNC_OK;
     CHECK_ARG(desc->n_in > 0 && desc->in && desc->coef && desc->out);
     int st = ctx->activate();
-    if (st) return st;
+    if (st || (st = ctx->note_capture())) return st;
     rlnc::MatmulParams p;
     matmul_desc_to_params(desc, p);
     return ctx->matmul(p);
@@ -412,26 +521,28 @@ static int encoder_from_host(rlnc_context *ctx, const uint8_t *data, size_t len,
         if (L * k != len) return RLNC_ERR_DATA_LENGTH_MISMATCH;  // :58-64
     }
     int st = ctx->activate();
-    if (st) return st;
+    if (st || (st = ctx->note_capture())) return st;
     std::unique_ptr<rlnc_encoder> e(new (std::nothrow) rlnc_encoder);
     if (!e) return set_error(RLNC_ERR_OUT_OF_MEMORY, "encoder allocation");
-    e->ctx = ctx;
+    e->bind(ctx);
     e->k = k;
     e->L = L;
     e->stride = round16(L);
     e->owned = true;
     HIP_TRY(hipMalloc(&e->src, k * e->stride));
+    Lease ws(ctx);
+    if ((st = ws.acquire())) return st;
     // padded image: data, 0x81 marker, zeros (encoder.rs:98-99), laid out at a 16-B row stride
-    if ((st = ctx->pin_a.ensure(k * e->stride))) return st;
-    uint8_t *h = ctx->pin_a.as<uint8_t>();
+    if ((st = ws->pin_a.ensure(k * e->stride))) return st;
+    uint8_t *h = ws->pin_a.as<uint8_t>();
     std::memset(h, 0, k * e->stride);
     for (size_t r = 0; r < k; ++r) {
         const size_t off = r * L;
         if (off < len) std::memcpy(h + r * e->stride, data + off, std::min(L, len - off));
     }
     if (pad) h[(len / L) * e->stride + (len % L)] = rlnc::kBoundaryMarker;
-    HIP_TRY(hipMemcpyAsync(e->src, h, k * e->stride, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpyAsync(e->src, h, k * e->stride, hipMemcpyHostToDevice, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
     *out = e.release();
     return RLNC_OK;
 }
@@ -453,7 +564,7 @@ int rlnc_encoder_from_device(rlnc_context *ctx, const uint8_t *pieces, size_t k,
     CHECK_ARG(pieces != nullptr && row_stride >= L);
     auto *e = new (std::nothrow) rlnc_encoder;
     if (!e) return set_error(RLNC_ERR_OUT_OF_MEMORY, "encoder allocation");
-    e->ctx = ctx;
+    e->bind(ctx);
     e->k = k;
     e->L = L;
     e->stride = row_stride;
@@ -463,11 +574,39 @@ int rlnc_encoder_from_device(rlnc_context *ctx, const uint8_t *pieces, size_t k,
     return RLNC_OK;
 }
 
+// #[derive(Clone)] (encoder.rs:18): an owned source is copied; a borrowed device source stays borrowed
+int rlnc_encoder_clone(const rlnc_encoder *e, rlnc_encoder **out) {
+    CHECK_ARG(e != nullptr && out != nullptr);
+    *out = nullptr;
+    int st = e->ctx->activate();
+    if (st) return st;
+    std::unique_ptr<rlnc_encoder> c(new (std::nothrow) rlnc_encoder);
+    if (!c) return set_error(RLNC_ERR_OUT_OF_MEMORY, "encoder allocation");
+    c->bind(e->ctx);
+    c->k = e->k;
+    c->L = e->L;
+    c->stride = e->stride;
+    c->owned = e->owned;
+    if (e->owned) {
+        HIP_TRY(hipMalloc(&c->src, e->k * e->stride));
+        Lease ws(e->ctx);
+        if ((st = ws.acquire())) return st;
+        HIP_TRY(hipMemcpyAsync(c->src, e->src, e->k * e->stride, hipMemcpyDeviceToDevice, ws->stream));
+        HIP_TRY(hipStreamSynchronize(ws->stream));
+    } else {
+        c->src = e->src;
+    }
+    *out = c.release();
+    return RLNC_OK;
+}
+
 void rlnc_encoder_free(rlnc_encoder *e) { delete e; }
 size_t rlnc_encoder_get_piece_count(const rlnc_encoder *e) { return e ? e->k : 0; }
 size_t rlnc_encoder_get_piece_byte_len(const rlnc_encoder *e) { return e ? e->L : 0; }
 size_t rlnc_encoder_get_full_coded_piece_byte_len(const rlnc_encoder *e) { return e ? e->k + e->L : 0; }
 
+// Thread-safe on one encoder (the reference's code(&self) on a Send + Sync Encoder): each call leases its own
+// stream and buffers.
 int rlnc_encoder_code_with_coding_vector(rlnc_encoder *e, const uint8_t *cv, size_t cv_len, uint8_t *coded,
                                          size_t coded_len) {
     CHECK_ARG(e != nullptr);
@@ -476,14 +615,16 @@ int rlnc_encoder_code_with_coding_vector(rlnc_encoder *e, const uint8_t *cv, siz
     CHECK_ARG(cv != nullptr && coded != nullptr);
     rlnc_context *ctx = e->ctx;
     int st = ctx->activate();
-    if (st) return st;
-    if ((st = ctx->ws_coef.ensure(e->k)) || (st = ctx->ws_out.ensure(e->L))) return st;
-    HIP_TRY(hipMemcpyAsync(ctx->ws_coef.p, cv, e->k, hipMemcpyHostToDevice, ctx->stream));
-    if ((st = encoder_launch(e, ctx->ws_coef.as<uint8_t>(), int64_t(e->k), 1, ctx->ws_out.as<uint8_t>(),
-                             int64_t(e->L), nullptr, 0)))
-        return st;
-    HIP_TRY(hipMemcpyAsync(coded, ctx->ws_out.p, e->L, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (st || (st = ctx->note_capture())) return st;
+    Lease ws(ctx);
+    if ((st = ws.acquire())) return st;
+    if ((st = ws->coef.ensure(e->k)) || (st = ws->out.ensure(e->L))) return st;
+    HIP_TRY(hipMemcpyAsync(ws->coef.p, cv, e->k, hipMemcpyHostToDevice, ws->stream));
+    const auto p = encoder_params(e, ws->coef.as<uint8_t>(), int64_t(e->k), 1, ws->out.as<uint8_t>(), int64_t(e->L),
+                                  nullptr, 0);
+    if ((st = ctx->matmul(p, ws->stream, ws->idx, false))) return st;
+    HIP_TRY(hipMemcpyAsync(coded, ws->out.p, e->L, hipMemcpyDeviceToHost, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
     return RLNC_OK;
 }
 
@@ -504,8 +645,9 @@ int rlnc_encoder_code_batch_device(rlnc_encoder *e, const uint8_t *coeffs_dev, s
     const size_t row = out_row_stride ? out_row_stride : e->k + e->L;
     CHECK_ARG(row >= e->k + e->L);
     int st = e->ctx->activate();
-    if (st) return st;
-    return encoder_launch(e, coeffs_dev, int64_t(e->k), int(n), out_dev + e->k, int64_t(row), out_dev, int64_t(row));
+    if (st || (st = e->ctx->note_capture())) return st;
+    return e->ctx->matmul(encoder_params(e, coeffs_dev, int64_t(e->k), int(n), out_dev + e->k, int64_t(row), out_dev,
+                                         int64_t(row)));
 }
 
 // ------------------------------------------------------------------------------------------------------
@@ -522,18 +664,42 @@ int rlnc_recoder_new(rlnc_context *ctx, const uint8_t *data, size_t len, size_t 
     if (n == 0) return RLNC_ERR_NOT_ENOUGH_PIECES_TO_RECODE;     // reference: UB (unwrap_unchecked, :97)
     CHECK_ARG(data != nullptr && n <= 0x7FFFFFFF);
     int st = ctx->activate();
-    if (st) return st;
+    if (st || (st = ctx->note_capture())) return st;
     std::unique_ptr<rlnc_recoder> r(new (std::nothrow) rlnc_recoder);
     if (!r) return set_error(RLNC_ERR_OUT_OF_MEMORY, "recoder allocation");
-    r->ctx = ctx;
+    r->bind(ctx);
     r->k = k;
     r->n = n;
     r->full = full;
     r->stride = round16(full);
     HIP_TRY(hipMalloc(&r->pieces, n * r->stride));
-    HIP_TRY(hipMemcpy2DAsync(r->pieces, r->stride, data, full, full, n, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    Lease ws(ctx);
+    if ((st = ws.acquire())) return st;
+    HIP_TRY(hipMemcpy2DAsync(r->pieces, r->stride, data, full, full, n, hipMemcpyHostToDevice, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
     *out = r.release();
+    return RLNC_OK;
+}
+
+// #[derive(Clone)] (recoder.rs:12)
+int rlnc_recoder_clone(const rlnc_recoder *r, rlnc_recoder **out) {
+    CHECK_ARG(r != nullptr && out != nullptr);
+    *out = nullptr;
+    int st = r->ctx->activate();
+    if (st) return st;
+    std::unique_ptr<rlnc_recoder> c(new (std::nothrow) rlnc_recoder);
+    if (!c) return set_error(RLNC_ERR_OUT_OF_MEMORY, "recoder allocation");
+    c->bind(r->ctx);
+    c->k = r->k;
+    c->n = r->n;
+    c->full = r->full;
+    c->stride = r->stride;
+    HIP_TRY(hipMalloc(&c->pieces, r->n * r->stride));
+    Lease ws(r->ctx);
+    if ((st = ws.acquire())) return st;
+    HIP_TRY(hipMemcpyAsync(c->pieces, r->pieces, r->n * r->stride, hipMemcpyDeviceToDevice, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
+    *out = c.release();
     return RLNC_OK;
 }
 
@@ -543,7 +709,8 @@ size_t rlnc_recoder_get_num_pieces_recoded_together(const rlnc_recoder *r) { ret
 size_t rlnc_recoder_get_piece_byte_len(const rlnc_recoder *r) { return r ? r->full - r->k : 0; }
 size_t rlnc_recoder_get_full_coded_piece_byte_len(const rlnc_recoder *r) { return r ? r->full : 0; }
 
-static int recoder_launch(rlnc_recoder *r, const uint8_t *r_dev, int count, uint8_t *out_dev, int64_t out_row) {
+static rlnc::MatmulParams recoder_params(const rlnc_recoder *r, const uint8_t *r_dev, int count, uint8_t *out_dev,
+                                         int64_t out_row) {
     // recoded piece = Σ_i r_i · (coeffs_i ‖ data_i): the coefficient fold of recoder.rs:133-144 and the
     // data combination of :146-150 are the same linear map applied to different columns
     rlnc::MatmulParams p{};
@@ -557,7 +724,7 @@ static int recoder_launch(rlnc_recoder *r, const uint8_t *r_dev, int count, uint
     p.n_in = int(r->n);
     p.width = int64_t(r->full);
     p.n_obj = 1;
-    return r->ctx->matmul(p);
+    return p;
 }
 
 int rlnc_recoder_recode_with_buf(rlnc_recoder *r, const uint8_t *rnd, size_t n_rnd, uint8_t *full, size_t full_len) {
@@ -567,12 +734,15 @@ int rlnc_recoder_recode_with_buf(rlnc_recoder *r, const uint8_t *rnd, size_t n_r
     CHECK_ARG(rnd != nullptr && full != nullptr);
     rlnc_context *ctx = r->ctx;
     int st = ctx->activate();
-    if (st) return st;
-    if ((st = ctx->ws_coef.ensure(r->n)) || (st = ctx->ws_out.ensure(r->full))) return st;
-    HIP_TRY(hipMemcpyAsync(ctx->ws_coef.p, rnd, r->n, hipMemcpyHostToDevice, ctx->stream));
-    if ((st = recoder_launch(r, ctx->ws_coef.as<uint8_t>(), 1, ctx->ws_out.as<uint8_t>(), int64_t(r->full)))) return st;
-    HIP_TRY(hipMemcpyAsync(full, ctx->ws_out.p, r->full, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (st || (st = ctx->note_capture())) return st;
+    Lease ws(ctx);
+    if ((st = ws.acquire())) return st;
+    if ((st = ws->coef.ensure(r->n)) || (st = ws->out.ensure(r->full))) return st;
+    HIP_TRY(hipMemcpyAsync(ws->coef.p, rnd, r->n, hipMemcpyHostToDevice, ws->stream));
+    const auto p = recoder_params(r, ws->coef.as<uint8_t>(), 1, ws->out.as<uint8_t>(), int64_t(r->full));
+    if ((st = ctx->matmul(p, ws->stream, ws->idx, false))) return st;
+    HIP_TRY(hipMemcpyAsync(full, ws->out.p, r->full, hipMemcpyDeviceToHost, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
     return RLNC_OK;
 }
 
@@ -581,8 +751,8 @@ int rlnc_recoder_recode_batch_device(rlnc_recoder *r, const uint8_t *r_dev, size
     if (count == 0) return RLNC_OK;
     CHECK_ARG(r_dev != nullptr && out_dev != nullptr && count <= 0x7FFFFFFF);
     int st = r->ctx->activate();
-    if (st) return st;
-    return recoder_launch(r, r_dev, int(count), out_dev, int64_t(r->full));
+    if (st || (st = r->ctx->note_capture())) return st;
+    return r->ctx->matmul(recoder_params(r, r_dev, int(count), out_dev, int64_t(r->full)));
 }
 
 // ------------------------------------------------------------------------------------------------------
@@ -594,50 +764,76 @@ int rlnc_decoder_new(rlnc_context *ctx, size_t L, size_t k, rlnc_decoder **out) 
     if (L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;  // decoder.rs:66-68
     if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;   // :69-71
     CHECK_ARG(k <= 0x7FFFFFFF);
-    auto *d = new (std::nothrow) rlnc_decoder;
+    std::unique_ptr<rlnc_decoder> d(new (std::nothrow) rlnc_decoder);
     if (!d) return set_error(RLNC_ERR_OUT_OF_MEMORY, "decoder allocation");
-    d->ctx = ctx;
+    d->bind(ctx);
     d->k = k;
     d->L = L;
     d->stride = round16(L);
-    d->elim.reset(new Elimination(k));
-    *out = d;
+    d->elim.reset(new (std::nothrow) Elimination(k));
+    if (!d->elim) return set_error(RLNC_ERR_OUT_OF_MEMORY, "decoder allocation");
+    *out = d.release();
+    return RLNC_OK;
+}
+
+// #[derive(Clone)] (decoder.rs:8): elimination state, counters and the stored data rows
+int rlnc_decoder_clone(const rlnc_decoder *d, rlnc_decoder **out) {
+    CHECK_ARG(d != nullptr && out != nullptr);
+    *out = nullptr;
+    int st = d->ctx->activate();
+    if (st) return st;
+    std::unique_ptr<rlnc_decoder> c(new (std::nothrow) rlnc_decoder);
+    if (!c) return set_error(RLNC_ERR_OUT_OF_MEMORY, "decoder allocation");
+    c->bind(d->ctx);
+    c->k = d->k;
+    c->L = d->L;
+    c->stride = d->stride;
+    c->received = d->received;
+    c->useful = d->useful;
+    c->elim.reset(new (std::nothrow) Elimination(*d->elim));
+    if (!c->elim) return set_error(RLNC_ERR_OUT_OF_MEMORY, "decoder allocation");
+    if (d->store_slots) {
+        HIP_TRY(hipMalloc(&c->store, d->store_slots * d->stride));
+        c->store_slots = d->store_slots;
+        Lease ws(d->ctx);
+        if ((st = ws.acquire())) return st;
+        HIP_TRY(hipMemcpyAsync(c->store, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ws->stream));
+        HIP_TRY(hipStreamSynchronize(ws->stream));
+    }
+    *out = c.release();
     return RLNC_OK;
 }
 
 void rlnc_decoder_free(rlnc_decoder *d) { delete d; }
 
-static int decoder_store_slot(rlnc_decoder *d, int slot, const uint8_t *src, hipMemcpyKind kind) {
-    rlnc_context *ctx = d->ctx;
+static int decoder_store_slot(rlnc_decoder *d, CallWs *ws, int slot, const uint8_t *src, hipMemcpyKind kind) {
     if (size_t(slot) >= d->store_slots) {
         size_t ns = std::max(d->elim->slots(), size_t(slot) + 1);
         uint8_t *n = nullptr;
         HIP_TRY(hipMalloc(&n, ns * d->stride));
         if (d->store) {
-            HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ctx->stream));
-            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ws->stream));
+            HIP_TRY(hipStreamSynchronize(ws->stream));
             (void)hipFree(d->store);
         }
         d->store = n;
         d->store_slots = ns;
     }
-    HIP_TRY(hipMemcpyAsync(d->store + size_t(slot) * d->stride, src, d->L, kind, ctx->stream));
-    if (kind == hipMemcpyHostToDevice) HIP_TRY(hipStreamSynchronize(ctx->stream));  // caller may reuse the piece
+    HIP_TRY(hipMemcpyAsync(d->store + size_t(slot) * d->stride, src, d->L, kind, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));  // the caller may reuse the piece; the call is synchronous
     return RLNC_OK;
 }
 
-static int decoder_decode_impl(rlnc_decoder *d, const uint8_t *coeffs_host, const uint8_t *data, hipMemcpyKind kind) {
+static int decoder_decode_impl(rlnc_decoder *d, CallWs *ws, const uint8_t *coeffs_host, const uint8_t *data,
+                               hipMemcpyKind kind) {
     int slot = -1;
     bool keep = false;
     const int st = d->elim->push(coeffs_host, &slot, &keep);
     if (st == RLNC_ERR_RECEIVED_ALL_PIECES) return st;
     d->received += 1;                                     // decoder.rs:107
     if (st == RLNC_OK) d->useful = d->elim->rank();       // :115
-    if (keep) {
-        int s2 = d->ctx->activate();
-        if (s2) return s2;
-        if ((s2 = decoder_store_slot(d, slot, data, kind))) return s2;
-    }
+    if (keep)
+        if (int s2 = decoder_store_slot(d, ws, slot, data, kind)) return s2;
     return st;
 }
 
@@ -646,7 +842,11 @@ int rlnc_decoder_decode(rlnc_decoder *d, const uint8_t *piece, size_t len) {
     if (d->elim->decoded()) return RLNC_ERR_RECEIVED_ALL_PIECES;  // decoder.rs:97-99
     if (len != d->k + d->L) return RLNC_ERR_INVALID_PIECE_LENGTH; // :100-102
     CHECK_ARG(piece != nullptr);
-    return decoder_decode_impl(d, piece, piece + d->k, hipMemcpyHostToDevice);
+    int st = d->ctx->activate();
+    if (st) return st;
+    Lease ws(d->ctx);
+    if ((st = ws.acquire())) return st;
+    return decoder_decode_impl(d, ws.ws.get(), piece, piece + d->k, hipMemcpyHostToDevice);
 }
 
 int rlnc_decoder_decode_device(rlnc_decoder *d, const uint8_t *piece_dev, size_t len) {
@@ -654,14 +854,14 @@ int rlnc_decoder_decode_device(rlnc_decoder *d, const uint8_t *piece_dev, size_t
     if (d->elim->decoded()) return RLNC_ERR_RECEIVED_ALL_PIECES;
     if (len != d->k + d->L) return RLNC_ERR_INVALID_PIECE_LENGTH;
     CHECK_ARG(piece_dev != nullptr);
-    rlnc_context *ctx = d->ctx;
-    int st = ctx->activate();
+    int st = d->ctx->activate();
     if (st) return st;
-    if ((st = ctx->pin_c.ensure(d->k))) return st;
-    HIP_TRY(hipMemcpyAsync(ctx->pin_c.p, piece_dev, d->k, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    std::vector<uint8_t> coeffs(ctx->pin_c.as<uint8_t>(), ctx->pin_c.as<uint8_t>() + d->k);
-    return decoder_decode_impl(d, coeffs.data(), piece_dev + d->k, hipMemcpyDeviceToDevice);
+    Lease ws(d->ctx);
+    if ((st = ws.acquire()) || (st = ws->pin_c.ensure(d->k))) return st;
+    HIP_TRY(hipMemcpyAsync(ws->pin_c.p, piece_dev, d->k, hipMemcpyDeviceToHost, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
+    std::vector<uint8_t> coeffs(ws->pin_c.as<uint8_t>(), ws->pin_c.as<uint8_t>() + d->k);
+    return decoder_decode_impl(d, ws.ws.get(), coeffs.data(), piece_dev + d->k, hipMemcpyDeviceToDevice);
 }
 
 int rlnc_decoder_is_already_decoded(const rlnc_decoder *d) { return d && d->elim->decoded() ? 1 : 0; }
@@ -672,22 +872,21 @@ size_t rlnc_decoder_get_received_piece_count(const rlnc_decoder *d) { return d ?
 size_t rlnc_decoder_get_useful_piece_count(const rlnc_decoder *d) { return d ? d->useful : 0; }
 size_t rlnc_decoder_get_remaining_piece_count(const rlnc_decoder *d) { return d ? d->k - d->useful : 0; }
 
-// decoded rows = T × stored data rows, written to out_dev [k][L]
-static int decoder_apply(rlnc_decoder *d, uint8_t *out_dev) {
-    rlnc_context *ctx = d->ctx;
+// decoded rows = T × stored data rows, written to out_dev [k][L] on the lease's stream
+static int decoder_apply(rlnc_decoder *d, CallWs *ws, uint8_t *out_dev) {
     const size_t slots = d->elim->slots();
     int st;
-    if ((st = ctx->pin_b.ensure(d->k * slots)) || (st = ctx->ws_coef.ensure(d->k * slots))) return st;
-    d->elim->transform(ctx->pin_b.as<uint8_t>(), slots);
-    HIP_TRY(hipMemcpyAsync(ctx->ws_coef.p, ctx->pin_b.p, d->k * slots, hipMemcpyHostToDevice, ctx->stream));
+    if ((st = ws->pin_b.ensure(d->k * slots)) || (st = ws->coef.ensure(d->k * slots))) return st;
+    d->elim->transform(ws->pin_b.as<uint8_t>(), slots);
+    HIP_TRY(hipMemcpyAsync(ws->coef.p, ws->pin_b.p, d->k * slots, hipMemcpyHostToDevice, ws->stream));
     if (d->store_slots < slots) {
         // slots never stored were never referenced; give them zero rows so T × D is well defined
         uint8_t *n = nullptr;
         HIP_TRY(hipMalloc(&n, slots * d->stride));
-        HIP_TRY(hipMemsetAsync(n, 0, slots * d->stride, ctx->stream));
+        HIP_TRY(hipMemsetAsync(n, 0, slots * d->stride, ws->stream));
         if (d->store)
-            HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
+            HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ws->stream));
+        HIP_TRY(hipStreamSynchronize(ws->stream));
         if (d->store) (void)hipFree(d->store);
         d->store = n;
         d->store_slots = slots;
@@ -695,7 +894,7 @@ static int decoder_apply(rlnc_decoder *d, uint8_t *out_dev) {
     rlnc::MatmulParams p{};
     p.in = d->store;
     p.in_row = int64_t(d->stride);
-    p.coef = ctx->ws_coef.as<uint8_t>();
+    p.coef = ws->coef.as<uint8_t>();
     p.coef_row = int64_t(slots);
     p.out = out_dev;
     p.out_row = int64_t(d->L);
@@ -703,20 +902,20 @@ static int decoder_apply(rlnc_decoder *d, uint8_t *out_dev) {
     p.n_in = int(slots);
     p.width = int64_t(d->L);
     p.n_obj = 1;
-    return ctx->matmul(p);
+    return d->ctx->matmul(p, ws->stream, ws->idx, false);
 }
 
 int rlnc_decoder_get_decoded_data(rlnc_decoder *d, uint8_t *out, size_t cap, size_t *out_len) {
     CHECK_ARG(d != nullptr);
     if (!d->elim->decoded()) return RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;  // decoder.rs:137-139
     CHECK_ARG(out != nullptr && out_len != nullptr && cap >= d->k * d->L);
-    rlnc_context *ctx = d->ctx;
-    int st = ctx->activate();
+    int st = d->ctx->activate();
     if (st) return st;
-    if ((st = ctx->ws_out.ensure(d->k * d->L))) return st;
-    if ((st = decoder_apply(d, ctx->ws_out.as<uint8_t>()))) return st;
-    HIP_TRY(hipMemcpyAsync(out, ctx->ws_out.p, d->k * d->L, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    Lease ws(d->ctx);
+    if ((st = ws.acquire()) || (st = ws->out.ensure(d->k * d->L))) return st;
+    if ((st = decoder_apply(d, ws.ws.get(), ws->out.as<uint8_t>()))) return st;
+    HIP_TRY(hipMemcpyAsync(out, ws->out.p, d->k * d->L, hipMemcpyDeviceToHost, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
     // get_final_data_len — decoder.rs:162-177: last nonzero byte must be the 0x81 marker, not at 0
     size_t n = d->k * d->L;
     while (n > 0 && out[n - 1] == 0) --n;
@@ -729,22 +928,23 @@ int rlnc_decoder_get_decoded_data_device(rlnc_decoder *d, uint8_t *out_dev, size
     CHECK_ARG(d != nullptr);
     if (!d->elim->decoded()) return RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;
     CHECK_ARG(out_dev != nullptr && out_len != nullptr && cap >= d->k * d->L);
-    rlnc_context *ctx = d->ctx;
-    int st = ctx->activate();
+    int st = d->ctx->activate();
     if (st) return st;
-    if ((st = decoder_apply(d, out_dev))) return st;
-    if ((st = ctx->ws_scan.ensure(8)) || (st = ctx->ws_status.ensure(4)) || (st = ctx->ws_len.ensure(8)) ||
-        (st = ctx->pin_c.ensure(16)))
+    Lease ws(d->ctx);
+    if ((st = ws.acquire())) return st;
+    if ((st = decoder_apply(d, ws.ws.get(), out_dev))) return st;
+    if ((st = ws->scan.ensure(8)) || (st = ws->status.ensure(4)) || (st = ws->len.ensure(8)) ||
+        (st = ws->pin_c.ensure(16)))
         return st;
-    HIP_TRY(rlnc::launch_final_data_len(out_dev, 0, int64_t(d->k * d->L), 1, ctx->ws_scan.as<unsigned long long>(),
-                                        ctx->ws_status.as<int32_t>(), ctx->ws_len.as<int64_t>(),
-                                        RLNC_ERR_INVALID_DECODED_DATA_FORMAT, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(ctx->pin_c.p, ctx->ws_status.p, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(ctx->pin_c.as<uint8_t>() + 8, ctx->ws_len.p, 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    const int32_t status = *ctx->pin_c.as<int32_t>();
+    HIP_TRY(rlnc::launch_final_data_len(out_dev, 0, int64_t(d->k * d->L), 1, ws->scan.as<unsigned long long>(),
+                                        ws->status.as<int32_t>(), ws->len.as<int64_t>(),
+                                        RLNC_ERR_INVALID_DECODED_DATA_FORMAT, ws->stream));
+    HIP_TRY(hipMemcpyAsync(ws->pin_c.p, ws->status.p, 4, hipMemcpyDeviceToHost, ws->stream));
+    HIP_TRY(hipMemcpyAsync(ws->pin_c.as<uint8_t>() + 8, ws->len.p, 8, hipMemcpyDeviceToHost, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
+    const int32_t status = *ws->pin_c.as<int32_t>();
     if (status) return status;
-    std::memcpy(out_len, ctx->pin_c.as<uint8_t>() + 8, 8);
+    std::memcpy(out_len, ws->pin_c.as<uint8_t>() + 8, 8);
     return RLNC_OK;
 }
 
@@ -759,7 +959,7 @@ static int encode_batch_impl(rlnc_context *ctx, const uint8_t *src, size_t k, si
     if (n == 0 || nobj == 0) return RLNC_OK;
     CHECK_ARG(src && coeffs && pieces && n <= 0x7FFFFFFF && k <= 0x7FFFFFFF && nobj <= 0x7FFFFFFF);
     int st = ctx->activate();
-    if (st) return st;
+    if (st || (st = ctx->note_capture())) return st;
     const int64_t full = int64_t(k + L);
     rlnc::MatmulParams p{};
     p.in = src;
@@ -799,7 +999,7 @@ int rlnc_encode_batch_headers(rlnc_context *ctx, const uint8_t *coeffs, size_t k
     if (n == 0 || nobj == 0) return RLNC_OK;
     CHECK_ARG(coeffs && pieces);
     int st = ctx->activate();
-    if (st) return st;
+    if (st || (st = ctx->note_capture())) return st;
     // pieces[o][i][0..k) = coeffs[o][i] (encoder.rs:246-248): one strided copy (a kernel: the runtime's 2D
     // blit took 36 µs for 1,024 rows of 32 B)
     HIP_TRY(rlnc::launch_copy_rows(pieces, int64_t(k + L), coeffs, int64_t(k), int64_t(k), int64_t(n * nobj),
@@ -816,7 +1016,7 @@ int rlnc_recode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t k, size_t
     if (count == 0 || nobj == 0) return RLNC_OK;
     CHECK_ARG(pieces && r && out && n <= 0x7FFFFFFF && count <= 0x7FFFFFFF && nobj <= 0x7FFFFFFF);
     int st = ctx->activate();
-    if (st) return st;
+    if (st || (st = ctx->note_capture())) return st;
     const int64_t full = int64_t(k + L);
     rlnc::MatmulParams p{};
     p.in = pieces;
@@ -864,7 +1064,7 @@ static int decode_apply_impl(rlnc_context *ctx, const uint8_t *pieces, size_t ob
                              int32_t *ostat_dev, int64_t *len_dev) {
     const size_t full = k + L;
     int st;
-    if ((st = ctx->ws_scan.ensure(nobj * 8))) return st;
+    if ((st = ctx->grow(ctx->ws_scan, nobj * 8))) return st;
     rlnc::MatmulParams p{};
     p.in = pieces + k;
     p.in_obj = int64_t(obj_stride);
@@ -889,7 +1089,7 @@ static int decode_batch_device_impl(rlnc_context *ctx, const uint8_t *pieces, si
                                     size_t m, size_t nobj, uint8_t *decoded, int32_t *pstat_dev, int32_t *ostat_dev,
                                     int64_t *len_dev, int32_t *rank_dev) {
     int st;
-    if ((st = ctx->ws_coef.ensure(nobj * k * m))) return st;
+    if ((st = ctx->grow(ctx->ws_coef, nobj * k * m))) return st;
     uint8_t *T = ctx->ws_coef.as<uint8_t>();
     if ((st = decode_eliminate_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, pstat_dev, rank_dev))) return st;
     return decode_apply_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, rank_dev, decoded, ostat_dev, len_dev);
@@ -902,7 +1102,7 @@ static int decode_batch_host_impl(rlnc_context *ctx, const uint8_t *pieces, size
     const size_t full = k + L;
     int st;
     // 1. coefficient headers → host (k bytes of each piece)
-    if ((st = ctx->pin_a.ensure(nobj * m * k))) return st;
+    if ((st = ctx->grow(ctx->pin_a, nobj * m * k))) return st;
     uint8_t *hdr = ctx->pin_a.as<uint8_t>();
     if (obj_stride == m * full) {
         HIP_TRY(hipMemcpy2DAsync(hdr, k, pieces, full, k, nobj * m, hipMemcpyDeviceToHost, ctx->stream));
@@ -913,7 +1113,7 @@ static int decode_batch_host_impl(rlnc_context *ctx, const uint8_t *pieces, size
     }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     // 2. exact incremental elimination per object (decoder.rs:96-118 for pieces 0..m-1), host threads
-    if ((st = ctx->pin_b.ensure(nobj * k * m))) return st;
+    if ((st = ctx->grow(ctx->pin_b, nobj * k * m))) return st;
     uint8_t *T = ctx->pin_b.as<uint8_t>();
     std::vector<int32_t> ranks(nobj, 0);
     std::vector<int32_t> pst(nobj * m, 0);
@@ -944,9 +1144,9 @@ static int decode_batch_host_impl(rlnc_context *ctx, const uint8_t *pieces, size
         for (auto &t : th) t.join();
     }
     // 3. T → device, decoded = T × received data rows (one launch for all objects)
-    if ((st = ctx->ws_coef.ensure(nobj * k * m)) || (st = ctx->ws_rank.ensure(nobj * 4)) ||
-        (st = ctx->ws_scan.ensure(nobj * 8)) || (st = ctx->ws_status.ensure(nobj * 4)) ||
-        (st = ctx->ws_len.ensure(nobj * 8)) || (st = ctx->pin_c.ensure(nobj * 16)))
+    if ((st = ctx->grow(ctx->ws_coef, nobj * k * m)) || (st = ctx->grow(ctx->ws_rank, nobj * 4)) ||
+        (st = ctx->grow(ctx->ws_scan, nobj * 8)) || (st = ctx->grow(ctx->ws_status, nobj * 4)) ||
+        (st = ctx->grow(ctx->ws_len, nobj * 8)) || (st = ctx->grow(ctx->pin_c, nobj * 16)))
         return st;
     HIP_TRY(hipMemcpyAsync(ctx->ws_coef.p, T, nobj * k * m, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(ctx->ws_rank.p, ranks.data(), nobj * 4, hipMemcpyHostToDevice, ctx->stream));
@@ -990,7 +1190,9 @@ static int decode_batch_check(rlnc_context *ctx, const uint8_t *pieces, size_t &
     CHECK_ARG(pieces && decoded && m > 0 && m <= 0x7FFFFFFF && k <= 0x7FFFFFFF && nobj <= 0x7FFFFFFF);
     if (obj_stride == 0) obj_stride = m * (k + L);
     CHECK_ARG(obj_stride >= m * (k + L));
-    return ctx->activate();
+    int st = ctx->activate();
+    if (st) return st;
+    return ctx->note_capture();
 }
 
 int rlnc_decode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L, size_t m,
@@ -1005,9 +1207,9 @@ int rlnc_decode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t obj_strid
     if (!fits || ctx->decode_path == 1)
         return decode_batch_host_impl(ctx, pieces, obj_stride, k, L, m, nobj, decoded, piece_status, object_status,
                                       data_len);
-    if ((st = ctx->ws_pstat.ensure(nobj * m * 4)) || (st = ctx->ws_status.ensure(nobj * 4)) ||
-        (st = ctx->ws_len.ensure(nobj * 8)) || (st = ctx->ws_rank.ensure(nobj * 4)) ||
-        (st = ctx->pin_c.ensure(nobj * (m * 4 + 16))))
+    if ((st = ctx->grow(ctx->ws_pstat, nobj * m * 4)) || (st = ctx->grow(ctx->ws_status, nobj * 4)) ||
+        (st = ctx->grow(ctx->ws_len, nobj * 8)) || (st = ctx->grow(ctx->ws_rank, nobj * 4)) ||
+        (st = ctx->grow(ctx->pin_c, nobj * (m * 4 + 16))))
         return st;
     if ((st = decode_batch_device_impl(ctx, pieces, obj_stride, k, L, m, nobj, decoded, ctx->ws_pstat.as<int32_t>(),
                                        ctx->ws_status.as<int32_t>(), ctx->ws_len.as<int64_t>(),
@@ -1036,7 +1238,7 @@ int rlnc_decode_batch_device(rlnc_context *ctx, const uint8_t *pieces, size_t ob
     if (rlnc::rref_lds_bytes(int(k), int(m)) > rlnc::kRrefMaxLds)
         return set_error(RLNC_ERR_INVALID_ARGUMENT, "k=%zu, m=%zu exceed the device elimination's LDS budget; use "
                          "rlnc_decode_batch", k, m);
-    if ((st = ctx->ws_rank.ensure(nobj * 4))) return st;
+    if ((st = ctx->grow(ctx->ws_rank, nobj * 4))) return st;
     return decode_batch_device_impl(ctx, pieces, obj_stride, k, L, m, nobj, decoded, piece_status_dev,
                                     object_status_dev, data_len_dev, ctx->ws_rank.as<int32_t>());
 }

@@ -23,6 +23,8 @@
 // then never waits on HBM.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include "../../include/rlnc_hip.h"
 #include "gf256.hpp"
 #include "kernels.hpp"
@@ -844,15 +846,25 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
         }  // k = 128 (<0, 1, 4, 1, 32>: 3.8 ms for 512 objects) stays on the one-wave LDS path (2.5 ms)
         if (mw && kern != &gf_rref_batch_kernel<0, 1, 1>) threads = 256;
     }
-    static bool attr_set = false;
-    if (!attr_set) {
-        for (auto f : {&gf_rref_batch_kernel<0, 1, 1>, &gf_rref_batch_kernel<4, 8, 1>, &gf_rref_batch_kernel<4, 8, 4, 4, 2>,
-                       &gf_rref_batch_kernel<2, 32, 1>, &gf_rref_batch_kernel<2, 32, 4, 2, 8>}) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(f),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, int(kRrefMaxLds));
-            if (e != hipSuccess) return e;
+    // the 160 KiB dynamic-LDS attribute, once per device (function attributes are per device), under a lock
+    {
+        static std::mutex mu;
+        static bool attr_set[64] = {};
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+        std::lock_guard<std::mutex> lock(mu);
+        if (!attr_set[dev]) {
+            for (auto f : {&gf_rref_batch_kernel<0, 1, 1>, &gf_rref_batch_kernel<4, 8, 1>,
+                           &gf_rref_batch_kernel<4, 8, 4, 4, 2>, &gf_rref_batch_kernel<2, 32, 1>,
+                           &gf_rref_batch_kernel<2, 32, 4, 2, 8>}) {
+                e = hipFuncSetAttribute(reinterpret_cast<const void *>(f),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(kRrefMaxLds));
+                if (e != hipSuccess) return e;
+            }
+            attr_set[dev] = true;
         }
-        attr_set = true;
     }
     hipLaunchKernelGGL(kern, dim3(p.n_obj), dim3(threads), lds, s, p, hdr_lds);
     return hipGetLastError();

@@ -82,6 +82,14 @@ class Encoder:
             self._lib.rlnc_encoder_free(self._h)
             self._h = None
 
+    def clone(self) -> "Encoder":
+        """#[derive(Clone)] (encoder.rs:18)."""
+        h = C.c_void_p()
+        check(self._lib.rlnc_encoder_clone(self._h, C.byref(h)), self._lib)
+        return Encoder(h, self._ctx)
+
+    __copy__ = clone
+
     def get_piece_count(self) -> int:
         return int(self._lib.rlnc_encoder_get_piece_count(self._h))
 
@@ -143,6 +151,14 @@ class Recoder:
             self._lib.rlnc_recoder_free(self._h)
             self._h = None
 
+    def clone(self) -> "Recoder":
+        """#[derive(Clone)] (recoder.rs:12)."""
+        h = C.c_void_p()
+        check(self._lib.rlnc_recoder_clone(self._h, C.byref(h)), self._lib)
+        return Recoder(h, self._ctx)
+
+    __copy__ = clone
+
     def get_original_num_pieces_coded_together(self) -> int:
         return int(self._lib.rlnc_recoder_get_original_num_pieces_coded_together(self._h))
 
@@ -199,6 +215,14 @@ class Decoder:
         if getattr(self, "_h", None):
             self._lib.rlnc_decoder_free(self._h)
             self._h = None
+
+    def clone(self) -> "Decoder":
+        """#[derive(Clone)] (decoder.rs:8): counters, elimination state and received rows."""
+        h = C.c_void_p()
+        check(self._lib.rlnc_decoder_clone(self._h, C.byref(h)), self._lib)
+        return Decoder(h, self._ctx)
+
+    __copy__ = clone
 
     def decode(self, full_coded_piece) -> None:
         """Decoder::decode — decoder.rs:96-118."""

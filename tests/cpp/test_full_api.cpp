@@ -4,6 +4,7 @@
 // Built and run by tests/test_gpu_cpp.py on the GPU box.
 #include <cstdio>
 #include <cstdlib>
+#include <thread>
 #include <vector>
 
 #include "rlnc/full.hpp"
@@ -142,6 +143,61 @@ void prop_encoder_recoder_decoder(uint64_t seed) {  // full/tests.rs:49-119 and 
     CHECK(out.is_ok() && out.value() == data);
 }
 
+void test_threads_and_clone() {
+    // An encoder built on a worker thread is used after that thread (and its thread-local context) has ended.
+    SplitMix rng(77);
+    const auto data = rng.bytes(40000);
+    Encoder e;
+    std::thread([&] { e = Encoder::create(data, 24).unwrap(); }).join();
+    auto d = Decoder::create(e.get_piece_byte_len(), e.get_piece_count()).unwrap();
+    while (!d.is_already_decoded()) {
+        auto r = d.decode(e.code(rng));
+        CHECK(r.is_ok() || r.error() == RLNCError::PieceNotUseful);
+    }
+    CHECK(d.get_decoded_data().value() == data);
+
+    // code(&self) from 8 threads at once on ONE encoder (the reference Encoder is Send + Sync): every piece equals
+    // the one a single thread computes afterwards from the same coefficient bytes.
+    const int nth = 8, per = 24;
+    std::vector<std::vector<std::vector<uint8_t>>> got(nth);
+    std::vector<std::thread> th;
+    for (int t = 0; t < nth; ++t)
+        th.emplace_back([&, t] {
+            SplitMix r(1000 + t);
+            for (int i = 0; i < per; ++i) got[t].push_back(e.code(r));
+        });
+    for (auto &t : th) t.join();
+    for (int t = 0; t < nth; ++t) {
+        SplitMix r(1000 + t);
+        for (int i = 0; i < per; ++i) CHECK(e.code(r) == got[t][i]);
+    }
+
+    // Clone: an encoder clone codes identically; a decoder cloned half-way finishes independently; a recoder
+    // clone recodes identically.
+    Encoder e2 = e.clone();
+    SplitMix ra(5), rb(5);
+    CHECK(e.code(ra) == e2.code(rb));
+    auto d1 = Decoder::create(e.get_piece_byte_len(), e.get_piece_count()).unwrap();
+    SplitMix rc(6);
+    std::vector<uint8_t> coded;
+    for (size_t i = 0; i < e.get_piece_count() / 2; ++i) {
+        auto p = e.code(rc);
+        CHECK(d1.decode(p).is_ok());
+        coded.insert(coded.end(), p.begin(), p.end());
+    }
+    Decoder d2 = d1;  // Clone
+    CHECK(d2.get_received_piece_count() == d1.get_received_piece_count() &&
+          d2.get_useful_piece_count() == d1.get_useful_piece_count());
+    SplitMix r1(8), r2(9);
+    while (!d1.is_already_decoded()) (void)d1.decode(e.code(r1));
+    while (!d2.is_already_decoded()) (void)d2.decode(e2.code(r2));
+    CHECK(d1.get_decoded_data().value() == data && d2.get_decoded_data().value() == data);
+    auto rec = Recoder::create(coded, e.get_full_coded_piece_byte_len(), e.get_piece_count()).unwrap();
+    Recoder rec2 = rec.clone();
+    SplitMix s1(11), s2(11);
+    CHECK(rec.recode(s1) == rec2.recode(s2));
+}
+
 }  // namespace
 
 int main() {
@@ -150,6 +206,7 @@ int main() {
     test_decoder();
     test_recoder();
     for (uint64_t s = 10; s < 14; ++s) prop_encoder_recoder_decoder(s);
+    test_threads_and_clone();
     std::printf("%s (%d failures)\n", g_fail ? "FAILED" : "all passed", g_fail);
     return g_fail ? 1 : 0;
 }

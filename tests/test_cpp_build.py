@@ -9,5 +9,5 @@ def test_cpp_mirror_compiles_and_links(tmp_path):
     exe = tmp_path / "t"
     subprocess.check_call(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"),
                            os.path.join(ROOT, "tests", "cpp", "test_full_api.cpp"), "-L" + os.path.join(ROOT, "rlnc_amd"),
-                           "-lrlnc_hip", "-o", str(exe)])
+                           "-lrlnc_hip", "-pthread", "-o", str(exe)])
     assert exe.exists()

@@ -80,3 +80,52 @@ def test_step_bytes_matches_reference_counters():
     assert bench.encode_counter(k, L) == 34_603_040
     assert bench.decode_counter(k, L) == 33_555_456
     assert bench.step_bytes(16, k, L, 64) == 16 * (64 * 34_603_040 + 33_555_456)
+
+
+def test_self_spawn_two_ranks_gloo():
+    """`bench.py --gpus 2` with no launcher starts its own 2 ranks (fresh interpreters, RANK/WORLD_SIZE/MASTER_*
+    set, rendezvous on 127.0.0.1) and rank 0 prints the one JSON line; here each rank's work is the C oracle
+    over gloo (--workload oracle-cpu), the GPU bench takes the same path over RCCL."""
+    import json
+    import subprocess
+    import sys
+
+    import bench
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py"), "--gpus", "2",
+                        "--workload", "oracle-cpu", "--steps", "3", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 3 and res["verified"]
+    assert res["total_bytes"] == 2 * bench.step_bytes(3, 8, 512, 12) * 3
+    assert abs(res["value"] - res["total_bytes"] / res["elapsed_s"] / bench.GIB) < 1e-3
+
+
+def test_self_spawn_stops_ranks_when_one_fails():
+    """A rank that dies before the rendezvous (test hook RLNC_BENCH_FAIL_RANK) makes the launcher stop the rank
+    left waiting in init_process_group and return the dead rank's exit code instead of hanging."""
+    import subprocess
+    import sys
+
+    import bench
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py"), "--gpus", "2",
+                        "--workload", "oracle-cpu", "--steps", "2"], capture_output=True, text=True, timeout=120,
+                       env=dict(env, RLNC_BENCH_FAIL_RANK="1"))
+    assert r.returncode == 5
+
+
+def test_config5_split_is_a_fixed_job():
+    import bench
+
+    a = bench.parse_args(["--workload", "config5"])
+    assert (a.k, a.piece_bytes, a.coded, a.decode_from, a.objects, a.chunk) == (128, 1 << 16, 128, 128, 4096, 512)
+    # objects per rank at N = 1..8 sum to the whole job
+    for n in (1, 2, 3, 4, 8):
+        per = [a.objects // n + (1 if r < a.objects % n else 0) for r in range(n)]
+        assert sum(per) == 4096

@@ -14,7 +14,7 @@ def test_cpp_api_mirror():
     os.makedirs(os.path.dirname(exe), exist_ok=True)
     subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-I" + os.path.join(ROOT, "include"),
                            os.path.join(ROOT, "tests", "cpp", "test_full_api.cpp"), "-L" + os.path.join(ROOT, "rlnc_amd"),
-                           "-lrlnc_hip", "-Wl,-rpath," + os.path.join(ROOT, "rlnc_amd"), "-o", exe])
+                           "-lrlnc_hip", "-Wl,-rpath," + os.path.join(ROOT, "rlnc_amd"), "-pthread", "-o", exe])
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "all passed" in r.stdout

@@ -48,6 +48,27 @@ cap.zero_()
 g.replay()
 torch.cuda.synchronize()
 assert torch.equal(cap, eager), "replay differs"
+# the captured graph holds the context's workspace addresses: a larger eager call on the same context must
+# refuse to grow them (instead of freeing memory the graph still writes), and the graph stays correct
+big_src = torch.from_numpy(rng.integers(0, 256, (4 * B, k, L), dtype=np.uint8)).cuda()
+big_co = torch.from_numpy(rng.integers(0, 256, (4 * B, n, k), dtype=np.uint8)).cuda()
+big = torch.zeros((4 * B, n, k + L), dtype=torch.uint8, device="cuda")
+try:
+    batch.encode_batch(big_src, big_co, big, ctx)
+    raise SystemExit("a workspace grew after a capture")
+except rlnc_amd.RLNCError as e:
+    assert e == rlnc_amd.RLNCError.InvalidArgument, e
+cap.zero_()
+g.replay()
+torch.cuda.synchronize()
+assert torch.equal(cap, eager), "replay after the refused call differs"
+ctx2 = rlnc_amd.Context(0)  # another context serves the larger shape
+batch.encode_batch(big_src, big_co, big, ctx2)
+ref = torch.zeros_like(big)
+ctx2.set_kernel_variant(0)
+batch.encode_batch(big_src, big_co, ref, ctx2)
+torch.cuda.synchronize()
+assert torch.equal(big, ref)
 print("graph ok")
 """
 
