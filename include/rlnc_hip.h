@@ -250,6 +250,53 @@ int rlnc_decode_batch_apply(rlnc_context *ctx, const uint8_t *pieces_dev, size_t
                             size_t L, size_t m, size_t num_objects, const uint8_t *T_dev, const int32_t *rank_dev,
                             uint8_t *decoded_dev, int32_t *object_status_dev, int64_t *data_len_dev);
 
+/* ---- wire formats on the device ------------------------------------------------------------
+ * Encoder::new's padded image (encoder.rs:85-106, BOUNDARY_MARKER consts.rs:5) built by a kernel from a byte
+ * string already in HBM: out[r][c] (r < k, c < L = ceil((data_len+1)/k), row stride out_row_stride, 0 = L) =
+ * data[r·L + c] below data_len, 0x81 at data_len, zeros after.  Errors as Encoder::new (DataLengthZero before
+ * PieceCountZero).  Asynchronous on the context stream; data may be unaligned. */
+typedef struct rlnc_pad_desc {
+    const uint8_t *data;
+    size_t data_len;
+    size_t k;
+    uint8_t *out;
+    size_t out_row_stride;
+} rlnc_pad_desc;
+size_t rlnc_padded_piece_byte_len(size_t data_len, size_t k); /* encoder.rs:93-95 (0 when k == 0) */
+int rlnc_pad_device(rlnc_context *ctx, const uint8_t *data_dev, size_t data_len, size_t k, uint8_t *out_dev,
+                    size_t out_row_stride);
+int rlnc_pad_batch_device(rlnc_context *ctx, const rlnc_pad_desc *descs, size_t count); /* one launch */
+/* Encoder::new from a device byte string: the encoder owns its padded image (built on the device). */
+int rlnc_encoder_new_device(rlnc_context *ctx, const uint8_t *data_dev, size_t data_len, size_t piece_count,
+                            rlnc_encoder **out);
+/* A ragged batch: every object with its own k, L, n and buffers (device pointers; strides 0 = dense), n coded
+ * pieces coeffs ‖ data each (encoder.rs:241-250).  Objects of one shape whose buffers sit at a constant object
+ * stride share a launch.  Asynchronous on the context stream. */
+typedef struct rlnc_object_desc {
+    const uint8_t *src;      /* k source pieces of L bytes */
+    size_t src_row_stride;   /* >= L, 0 = L */
+    const uint8_t *coeffs;   /* n × k coding vectors */
+    uint8_t *pieces;         /* n full coded pieces */
+    size_t piece_row_stride; /* >= k + L, 0 = k + L */
+    size_t k, L, n;
+} rlnc_object_desc;
+int rlnc_encode_ragged(rlnc_context *ctx, const rlnc_object_desc *objs, size_t count);
+
+/* ---- host-resident pieces (a socket or a file) ---------------------------------------------
+ * The batch API above for host buffers: objects stream through the device in windows of `window` objects (0 =
+ * automatic, >= 64 MiB of input per window), three pipeline slots with their own streams so that window w+1's
+ * host-to-device copy, window w's encode/decode and window w-1's device-to-host copy overlap.  Pinned host buffers
+ * (hipHostMalloc / hipHostRegister) are copied by DMA directly; pageable ones are staged through pinned buffers by
+ * host threads.  Same results as the device-resident calls (they run them).  Synchronous. */
+/* src [obj][k][L], coeffs [obj][n][k] → pieces [obj][n][k+L] (rlnc_encode_batch). */
+int rlnc_encode_host_stream(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t num_objects,
+                            const uint8_t *coeffs, size_t n, uint8_t *pieces, size_t window);
+/* pieces: the first m pieces of each object (object stride in bytes, 0 = m*(k+L)) → decoded [obj][k][L], host
+ * statuses as rlnc_decode_batch (each may be NULL). */
+int rlnc_decode_host_stream(rlnc_context *ctx, const uint8_t *pieces, size_t pieces_obj_stride, size_t k, size_t L,
+                            size_t m, size_t num_objects, uint8_t *decoded, int32_t *piece_status,
+                            int32_t *object_status, uint64_t *data_len, size_t window);
+
 /* ---- host-only: the decoder's exact coefficient elimination (no device needed) ---------------------------
  * The diagonal-pivot RREF of DecoderMatrix (decoder_matrix.rs:99-244) replicated on [coeffs | E] where E
  * tracks every row as a combination of received pieces; data rows = E × received data (elimination.hpp).

@@ -20,6 +20,16 @@ szp = C.POINTER(C.c_size_t)
 vp = C.c_void_p
 
 
+class PadDesc(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("data_len", C.c_size_t), ("k", C.c_size_t), ("out", C.c_void_p),
+                ("out_row_stride", C.c_size_t)]
+
+
+class ObjectDesc(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("src_row_stride", C.c_size_t), ("coeffs", C.c_void_p), ("pieces", C.c_void_p),
+                ("piece_row_stride", C.c_size_t), ("k", C.c_size_t), ("L", C.c_size_t), ("n", C.c_size_t)]
+
+
 class MatmulDesc(C.Structure):
     _fields_ = [
         ("in_", C.c_void_p), ("in_obj_stride", C.c_int64), ("in_row_stride", C.c_int64),
@@ -94,6 +104,15 @@ _SIGS = {
                                     i32p, u64p]),
     "rlnc_decode_batch_device": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp,
                                            vp, vp, vp]),
+    "rlnc_padded_piece_byte_len": (C.c_size_t, [C.c_size_t, C.c_size_t]),
+    "rlnc_pad_device": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, vp, C.c_size_t]),
+    "rlnc_pad_batch_device": (C.c_int, [vp, vp, C.c_size_t]),
+    "rlnc_encoder_new_device": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.POINTER(vp)]),
+    "rlnc_encode_ragged": (C.c_int, [vp, vp, C.c_size_t]),
+    "rlnc_encode_host_stream": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, vp, C.c_size_t, vp,
+                                          C.c_size_t]),
+    "rlnc_decode_host_stream": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp,
+                                          i32p, i32p, u64p, C.c_size_t]),
     "rlnc_elimination_new": (C.c_int, [C.c_size_t, C.c_size_t, C.POINTER(vp)]),
     "rlnc_elimination_free": (None, [vp]),
     "rlnc_elimination_push": (C.c_int, [vp, vp, i32p, i32p]),

@@ -1,0 +1,250 @@
+// context.hpp — librlnc_hip internals shared by engine.cpp, host_stream.cpp and wire.cpp: error reporting, the
+// grow-only device / pinned buffers, the per-call workspace pool and struct rlnc_context (include/rlnc_hip.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/rlnc_hip.h"
+#include "kernels.hpp"
+
+namespace rlnc::eng {
+
+extern thread_local std::string g_last_error;
+
+inline int set_error(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                    \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess) {                                                                          \
+            return ::rlnc::eng::set_error(e_ == hipErrorOutOfMemory ? RLNC_ERR_OUT_OF_MEMORY : RLNC_ERR_DEVICE, \
+                                          "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                                          __LINE__);                                                     \
+        }                                                                                                \
+    } while (0)
+
+#define CHECK_ARG(cond)                                                                                     \
+    do {                                                                                                    \
+        if (!(cond)) return ::rlnc::eng::set_error(RLNC_ERR_INVALID_ARGUMENT, "invalid argument: %s", #cond); \
+    } while (0)
+
+inline size_t round16(size_t v) { return (v + 15) & ~size_t(15); }
+
+// grow-only device buffer
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return RLNC_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        HIP_TRY(hipMalloc(&p, std::max<size_t>(bytes, 256)));
+        cap = std::max<size_t>(bytes, 256);
+        return RLNC_OK;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    template <class T>
+    T *as() const {
+        return static_cast<T *>(p);
+    }
+};
+
+// grow-only pinned host buffer
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return RLNC_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        HIP_TRY(hipHostMalloc(&p, std::max<size_t>(bytes, 256), hipHostMallocDefault));
+        cap = std::max<size_t>(bytes, 256);
+        return RLNC_OK;
+    }
+    ~PinBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    template <class T>
+    T *as() const {
+        return static_cast<T *>(p);
+    }
+};
+
+
+// Workspace of one object-API call (Encoder/Recoder/Decoder on host buffers): its own stream, scratch and
+// staging buffers, leased from the context's pool for the duration of the call.  Concurrent calls on one
+// context (e.g. Encoder::code(&self) from many threads, encoder.rs:264 -- the reference type is Send + Sync)
+// therefore never share a buffer.
+struct CallWs {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev = nullptr;
+    DevBuf coef, out, idx, scan, status, len;
+    PinBuf pin_a, pin_b, pin_c;
+    ~CallWs() {
+        if (ev) (void)hipEventDestroy(ev);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+}  // namespace rlnc::eng
+
+using rlnc::eng::set_error;
+
+struct rlnc_context {
+    using DevBuf = rlnc::eng::DevBuf;
+    using PinBuf = rlnc::eng::PinBuf;
+    using CallWs = rlnc::eng::CallWs;
+    std::atomic<int> refs{1};  // the creator's reference + one per Encoder/Decoder/Recoder bound to it
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    rlnc::MatmulVariant variant = rlnc::MatmulVariant::BitSlicedJumpShared8;
+    int max_tile_rows = 0;
+    int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination,
+                          // 3 device elimination with the clean state on LDS, 4 ... on one wave's
+                          // registers (A/B)
+    // workspaces of the stream-ordered batch / _device API (one caller thread per context at a time)
+    DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len, ws_pstat, ws_rank, ws_idx;
+    PinBuf pin_a, pin_b, pin_c;
+    // set once a batch call ran inside a HIP stream capture: the graph holds the workspace addresses, so
+    // they must never move again (grow() refuses instead of reallocating)
+    std::atomic<bool> graph_bound{false};
+    std::mutex pool_mu;
+    std::vector<std::unique_ptr<CallWs>> pool;
+    std::vector<rlnc_context *> subs;  // per-slot sub-contexts of the host-stream pipeline (host_stream.cpp)
+    DevBuf hs_din, hs_dcoef, hs_dout, hs_dst;  // as a host-stream slot: window buffers, kept between calls
+    PinBuf hs_hin, hs_hout, hs_hst;
+    DevBuf ws_tab;  // descriptor tables of the wire-format calls (wire.hip), uploaded from pin_tab
+    PinBuf pin_tab;
+    hipEvent_t tab_ev = nullptr;  // the last descriptor upload (pin_tab may be rewritten once it has run)
+
+    int sub_context(size_t i, rlnc_context **out);
+    void retain() { refs.fetch_add(1, std::memory_order_relaxed); }
+    void release() {
+        if (refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+        for (rlnc_context *c : subs)
+            if (c) c->release();
+        (void)hipSetDevice(device);
+        (void)hipStreamSynchronize(stream);
+        if (tab_ev) (void)hipEventDestroy(tab_ev);
+        if (own) (void)hipStreamDestroy(own);
+        delete this;  // the buffers' destructors free on this device
+    }
+    int activate() const {
+        HIP_TRY(hipSetDevice(device));
+        return RLNC_OK;
+    }
+    // batch API: note a stream capture in progress (freezes the workspaces)
+    int note_capture() {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_TRY(hipStreamIsCapturing(stream, &cs));
+        if (cs != hipStreamCaptureStatusNone) graph_bound = true;
+        return RLNC_OK;
+    }
+    int grow(DevBuf &b, size_t bytes) {
+        if (bytes <= b.cap) return RLNC_OK;
+        if (graph_bound)
+            return set_error(RLNC_ERR_INVALID_ARGUMENT,
+                             "this context's workspaces are bound to a captured HIP graph and cannot grow to %zu "
+                             "bytes: capture the largest shape first, or use another context",
+                             bytes);
+        return b.ensure(bytes);
+    }
+    int grow(PinBuf &b, size_t bytes) {
+        if (bytes <= b.cap) return RLNC_OK;
+        if (graph_bound)
+            return set_error(RLNC_ERR_INVALID_ARGUMENT,
+                             "this context's workspaces are bound to a captured HIP graph and cannot grow");
+        return b.ensure(bytes);
+    }
+    // a call workspace, ordered after the work already enqueued on the context stream
+    int lease(std::unique_ptr<CallWs> &ws) {
+        {
+            std::lock_guard<std::mutex> lock(pool_mu);
+            if (!pool.empty()) {
+                ws = std::move(pool.back());
+                pool.pop_back();
+            }
+        }
+        if (!ws) {
+            ws.reset(new (std::nothrow) CallWs);
+            if (!ws) return set_error(RLNC_ERR_OUT_OF_MEMORY, "call workspace allocation");
+            HIP_TRY(hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&ws->ev, hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventRecord(ws->ev, stream));
+        HIP_TRY(hipStreamWaitEvent(ws->stream, ws->ev, 0));
+        return RLNC_OK;
+    }
+    void unlease(std::unique_ptr<CallWs> ws) {
+        if (!ws) return;
+        std::lock_guard<std::mutex> lock(pool_mu);
+        pool.push_back(std::move(ws));
+    }
+    // the GF(2^8) matmul on stream s with index scratch idx (batch API: the context's; object API: the lease's)
+    int matmul(rlnc::MatmulParams p, hipStream_t s, DevBuf &idx, bool batch) {
+        if (max_tile_rows > 0 && p.n_out > max_tile_rows) {
+            // split the output rows into launches of at most max_tile_rows rows (tuning knob)
+            const int total = p.n_out;
+            for (int r0 = 0; r0 < total; r0 += max_tile_rows) {
+                rlnc::MatmulParams q = p;
+                q.n_out = std::min(max_tile_rows, total - r0);
+                q.coef = p.coef + int64_t(r0) * p.coef_row;
+                q.out = p.out + int64_t(r0) * p.out_row;
+                if (p.hdr) q.hdr = p.hdr + int64_t(r0) * p.hdr_row;
+                if (int st = launch(q, s, idx, batch)) return st;
+            }
+            return RLNC_OK;
+        }
+        return launch(p, s, idx, batch);
+    }
+    int matmul(const rlnc::MatmulParams &p) { return matmul(p, stream, ws_idx, true); }
+    int launch(const rlnc::MatmulParams &p, hipStream_t s, DevBuf &idx, bool batch) {
+        const rlnc::MatmulVariant v = variant;
+        const size_t need = rlnc::matmul_scratch_bytes(p, v);
+        if (need)
+            if (int st = batch ? grow(idx, need) : idx.ensure(need)) return st;
+        HIP_TRY(rlnc::launch_matmul(p, s, v, idx.p, idx.cap));
+        return RLNC_OK;
+    }
+};
+
+namespace rlnc::eng {
+// RAII lease of a call workspace
+struct Lease {
+    rlnc_context *ctx;
+    std::unique_ptr<CallWs> ws;
+    explicit Lease(rlnc_context *c) : ctx(c) {}
+    int acquire() { return ctx->lease(ws); }
+    CallWs *operator->() const { return ws.get(); }
+    ~Lease() { ctx->unlease(std::move(ws)); }
+};
+}  // namespace rlnc::eng
+
+struct rlnc_encoder;
+namespace rlnc::eng {
+// an Encoder owning the padded image img (k rows of L bytes at `stride`, hipMalloc'd; freed with the encoder)
+int encoder_adopt_device(rlnc_context *ctx, uint8_t *img, size_t k, size_t L, size_t stride, rlnc_encoder **out);
+}  // namespace rlnc::eng

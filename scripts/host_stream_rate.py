@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Host-resident rate of the library's own streaming API.
+
+Same per-object workload as bench.py (encode k=32 × 1 MiB → 64 coded pieces, decode from the first 32), but every
+object starts and ends in host memory and crosses PCIe through librlnc_hip's pipeline:
+    rlnc_encode_host_stream: source (host) → 64 coded pieces (host)
+    rlnc_decode_host_stream: the first 32 coded pieces of each object (host, strided) → decoded rows (host)
+once with pinned host buffers (DMA straight from/to them) and once with pageable ones (staged through the
+library's pinned buffers by host threads).  Reports GiB/s in bench.py's counters, the PCIe bytes moved, the raw
+pinned copy rates of the box, and checks decoded == source for every object.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--objects", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--window", type=int, default=0, help="objects per pipeline window (0 = library default)")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import bench
+    import rlnc_amd
+
+    k, L, n, m, B = 32, 1 << 20, 64, 32, args.objects
+    ctx = rlnc_amd.Context(0)
+    lib = ctx.lib
+    rng = np.random.default_rng(1)
+    out = {"metric": "host-resident RLNC encode+decode GiB/s (library pipeline, host buffers in and out), "
+                     "k=32 x 1 MiB", "unit": "GiB/s", "objects": B}
+    for mode in ("pinned", "pageable"):
+        pin = mode == "pinned"
+
+        def buf(shape):
+            return torch.empty(shape, dtype=torch.uint8, pin_memory=pin)
+
+        src, co, pieces, dec = buf((B, k, L)), buf((B, n, k)), buf((B, n, k + L)), buf((B, k, L))
+        src.numpy()[...] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+        co.numpy()[...] = rng.integers(0, 256, (B, n, k), dtype=np.uint8)
+        ps = np.zeros((B, m), np.int32)
+        os_ = np.zeros(B, np.int32)
+        dl = np.zeros(B, np.uint64)
+        p = lambda t: C.c_void_p(t.data_ptr())
+
+        def step():
+            assert lib.rlnc_encode_host_stream(ctx.h, p(src), k, L, B, p(co), n, p(pieces), args.window) == 0
+            assert lib.rlnc_decode_host_stream(ctx.h, p(pieces), n * (k + L), k, L, m, B, p(dec),
+                                               ps.ctypes.data_as(C.POINTER(C.c_int32)),
+                                               os_.ctypes.data_as(C.POINTER(C.c_int32)),
+                                               dl.ctypes.data_as(C.POINTER(C.c_uint64)), args.window) == 0
+
+        step()  # warm-up: the library's pipeline buffers are allocated once and kept
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        el = (time.perf_counter() - t0) / args.steps
+        ok = all((ps[o] == 0).sum() < k or np.array_equal(dec.numpy()[o], src.numpy()[o]) for o in range(B))
+        moved = B * (k * L + n * k + n * (k + L) + m * (k + L) + k * L)
+        out[mode] = {"value": round(bench.step_bytes(B, k, L, n) / el / 2**30, 2), "ms_per_step": round(el * 1e3, 2),
+                     "pcie_bytes_per_step": moved, "pcie_GBps_effective": round(moved / el / 1e9, 2),
+                     "roundtrip_goodput_GiBps": round(B * k * L / el / 2**30, 3), "verified": bool(ok)}
+        del src, co, pieces, dec
+    # raw pinned copy rates of this box
+    big_h = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+    big_d = torch.empty(1 << 30, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    big_d.copy_(big_h, non_blocking=True)
+    torch.cuda.synchronize()
+    out["pinned_h2d_GBps"] = round((1 << 30) / (time.perf_counter() - t) / 1e9, 2)
+    t = time.perf_counter()
+    big_h.copy_(big_d, non_blocking=True)
+    torch.cuda.synchronize()
+    out["pinned_d2h_GBps"] = round((1 << 30) / (time.perf_counter() - t) / 1e9, 2)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
