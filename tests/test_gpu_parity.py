@@ -184,9 +184,11 @@ def test_matmul_every_coefficient(ctx, variant):
     assert np.array_equal(got[0], np_matmul(coef[0], inp[0]))
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7])
-def test_matmul_bitsliced_strided_with_header(ctx, variant):
-    """Padded row strides and the coded-piece header copy, through the raw C ABI descriptor."""
+@pytest.mark.parametrize("variant", [5, 6, 7, 8])
+@pytest.mark.parametrize("n_out", [12, 40, 70])
+def test_matmul_bitsliced_strided_with_header(ctx, variant, n_out):
+    """Padded row strides and the coded-piece header copy, through the raw C ABI descriptor; n_out > 32 reaches
+    variant 8's 64-row, 8-wave tile (and its ragged second tile at 70)."""
     import ctypes as C
 
     import torch
@@ -194,8 +196,8 @@ def test_matmul_bitsliced_strided_with_header(ctx, variant):
     from rlnc_amd import _lib
     from rlnc_amd.errors import check
 
-    rng = np.random.default_rng(5)
-    nobj, n_out, n_in, W, pad = 2, 12, 20, 16384 * 2 + 32, 48
+    rng = np.random.default_rng(5 + n_out)
+    nobj, n_in, W, pad = 2, 20, 16384 * 2 + 32, 48
     hdr_w = n_in
     coef = rng.integers(0, 256, (nobj, n_out, n_in), dtype=np.uint8)
     inp = rng.integers(0, 256, (nobj, n_in, W + pad), dtype=np.uint8)
