@@ -272,6 +272,26 @@ def xor3_ceiling() -> dict | None:
                    "multiply-adds per XOR3 (8 XOR3s add c·x into the 8 bit-planes of 64 lanes × 32 bytes)"}
 
 
+def hbm_ceiling(objects: int, k: int, L: int) -> dict | None:
+    """HBM rates of this box with no GF arithmetic (measure/hbm_ceiling.hip): a float4 copy, a contiguous read and
+    the single-pass encoder's own access pattern (k rows of one 4 KiB column block per workgroup, XOR for the
+    product).  None if the microbenchmark is not built."""
+    path = os.path.join(ROOT, "measure", "libhbm_ceiling.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.hbm_rates.restype = ctypes.c_int
+    lib.hbm_rates.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_longlong, ctypes.POINTER(ctypes.c_double)]
+    r = (ctypes.c_double * 4)()
+    if lib.hbm_rates(objects, k, L, r) != 0:
+        return None
+    return {"copy_GBps": round(r[0], 1), "read_GBps": round(r[1], 1), "pattern_read_GBps": round(r[2], 1),
+            "pattern_compulsory_GBps": round(r[3], 1),
+            "how": f"measure/hbm_ceiling.hip over {objects} x {k} x {L} B (> the 256 MiB Infinity Cache): 16-B/lane "
+                   "copy (read+write bytes), contiguous read, and the single-pass encode's access pattern with XOR "
+                   "in place of the GF product; median of 7 launches"}
+
+
 # ------------------------------------------------------------------------------------------------------
 # GPU run
 # ------------------------------------------------------------------------------------------------------
@@ -619,10 +639,14 @@ def run_gpu(args, dist: Dist):
         S0 = sets[0]  # holds the timed encode of chunk 0 (config2 has one launch group per step)
         ok1 = S0["obj"] == (c0, c1) and torch.equal(out1[:, 0, k:], S0["pieces"][: c1 - c0, 0, k:])
         read1 = (c1 - c0) * (k * L + k)
-        single = {"coded_per_pass": 1, "kernel": "gf_matmul_stream_kernel<1, 2>", "ms": round(ms1, 4),
+        single = {"coded_per_pass": 1, "kernel": "gf_matmul_stream3_kernel<1, 1, 2, true>", "ms": round(ms1, 4),
                   "source_read_GBps": round(read1 / ms1 / 1e6, 1),
                   "read_frac": round(read1 / ms1 / 1e6 / HBM_PEAK_GBS, 4),
                   "compulsory_GBps": round((read1 + (c1 - c0) * (k + L)) / ms1 / 1e6, 1), "verified": bool(ok1)}
+        hc = None if args.no_ceiling else hbm_ceiling(c1 - c0, k, L)
+        if hc:
+            single["ceiling"] = hc
+            single["frac_of_pattern_ceiling"] = round(read1 / ms1 / 1e6 / hc["pattern_read_GBps"], 4)
 
     result = {
         "metric": METRIC,

@@ -19,6 +19,7 @@
 // north-star's literal design; it is kept as the ablation baseline.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 
 #include "../../include/rlnc_hip.h"
@@ -230,6 +231,10 @@ __device__ __forceinline__ uint4 ld16_nt(const uint8_t *ptr) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+#ifndef RLNC_STREAM_FORM_DEFAULT
+#define RLNC_STREAM_FORM_DEFAULT 11  // stream3<PF 1, VW 2, 64-bit shifts>: profiles/r02_stream_ab.txt
+#endif
+
 template <int NT, int PF>
 __global__ __launch_bounds__(kThreads) void gf_matmul_stream_kernel(MatmulParams p, int row_tiles, int col_blocks) {
     __shared__ uint4 s_t01[kKC][NT];
@@ -285,12 +290,141 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_stream_kernel(MatmulParams
     copy_header(p, t);
 }
 
+// Selectors from 64-bit shifts: one v_lshrrev_b64 shifts two dwords; the bits that cross the dword boundary land
+// in bits 29-31 (>> 3) or 26-31 (>> 6) of the low dword's top byte, which the masks clear.
+__device__ __forceinline__ Sel selectors64(uint4 x) {
+    Sel s;
+    const uint64_t a = (uint64_t(x.y) << 32) | x.x, b = (uint64_t(x.w) << 32) | x.z;
+    uint64_t a3, b3, a6, b6;  // the compiler splits a C++ 64-bit shift into 32-bit ones: ask for the pair form
+    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(a3) : "v"(a));
+    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(b3) : "v"(b));
+    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(a6) : "v"(a));
+    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(b6) : "v"(b));
+    s.s0[0] = x.x & 0x07070707u;
+    s.s0[1] = x.y & 0x07070707u;
+    s.s0[2] = x.z & 0x07070707u;
+    s.s0[3] = x.w & 0x07070707u;
+    s.s1[0] = uint32_t(a3) & 0x07070707u;
+    s.s1[1] = uint32_t(a3 >> 32) & 0x07070707u;
+    s.s1[2] = uint32_t(b3) & 0x07070707u;
+    s.s1[3] = uint32_t(b3 >> 32) & 0x07070707u;
+    s.s2[0] = uint32_t(a6) & 0x03030303u;
+    s.s2[1] = uint32_t(a6 >> 32) & 0x03030303u;
+    s.s2[2] = uint32_t(b6) & 0x03030303u;
+    s.s2[3] = uint32_t(b6 >> 32) & 0x03030303u;
+    return s;
+}
+
+// One-block streaming form with VW 16-byte slots per lane (slot v at column v * 4 KiB of a VW * 4 KiB block:
+// every table read feeds VW x the bytes, VW x PF loads in flight per lane) and optionally 64-bit-shift selectors.
+template <int NT, int PF, int VW, bool SH64>
+__global__ __launch_bounds__(kThreads) void gf_matmul_stream3_kernel(MatmulParams p, int row_tiles, int col_blocks) {
+    __shared__ uint4 s_t01[kKC][NT];
+    __shared__ uint32_t s_t2[kKC][NT];
+    int rt, cb, obj;
+    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    const int row0 = rt * NT;
+    const int rows_here = min(NT, p.n_out - row0);
+    const int kc = p.n_in;
+    const uint8_t *rowp = p.in + int64_t(obj) * p.in_obj + int64_t(cb) * kColBlock * VW + threadIdx.x * kBytesPerThread;
+    uint4 buf[PF][VW];
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+#pragma unroll
+        for (int v = 0; v < VW; ++v) buf[u][v] = ld16_nt(rowp + int64_t(min(u, kc - 1)) * p.in_row + v * kColBlock);
+    const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
+    for (int e = threadIdx.x; e < kKC * NT; e += kThreads) {
+        const int i = e % NT, j = e / NT;
+        const uint8_t c = (i < rows_here && j < kc) ? coef_base[int64_t(i) * p.coef_row + j] : uint8_t(0);
+        const PermTable pt = make_perm_table(c);
+        s_t01[j][i] = make_uint4(pt.t0lo, pt.t0hi, pt.t1lo, pt.t1hi);
+        s_t2[j][i] = pt.t2;
+    }
+    __syncthreads();
+    uint32_t acc[NT][VW][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int v = 0; v < VW; ++v) acc[i][v][0] = acc[i][v][1] = acc[i][v][2] = acc[i][v][3] = 0u;
+    for (int jb = 0; jb < kc; jb += PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int j = jb + u;
+            if (j >= kc) break;
+            Sel a[VW];
+#pragma unroll
+            for (int v = 0; v < VW; ++v) {
+                a[v] = SH64 ? selectors64(buf[u][v]) : selectors(buf[u][v]);
+                buf[u][v] = ld16_nt(rowp + int64_t(min(j + PF, kc - 1)) * p.in_row + v * kColBlock);
+            }
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                const uint4 ta = s_t01[j][i];
+                const uint32_t ta2 = s_t2[j][i];
+#pragma unroll
+                for (int v = 0; v < VW; ++v)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        acc[i][v][q] = xor3(xor3(acc[i][v][q], vperm(ta.y, ta.x, a[v].s0[q]), vperm(ta.w, ta.z, a[v].s1[q])),
+                                            vperm(ta2, ta2, a[v].s2[q]), 0u);
+            }
+        }
+    }
+    uint8_t *outp = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + int64_t(cb) * kColBlock * VW +
+                    threadIdx.x * kBytesPerThread;
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+        if (i < rows_here)
+#pragma unroll
+            for (int v = 0; v < VW; ++v)
+                *reinterpret_cast<uint4 *>(outp + int64_t(i) * p.out_row + v * kColBlock) =
+                    make_uint4(acc[i][v][0], acc[i][v][1], acc[i][v][2], acc[i][v][3]);
+    if (p.hdr != nullptr && cb == 0) {
+        uint8_t *h = p.hdr + int64_t(obj) * p.hdr_obj + int64_t(row0) * p.hdr_row;
+        for (int e = threadIdx.x; e < rows_here * p.n_in; e += kThreads) {
+            const int i = e / p.n_in, jj = e % p.n_in;
+            h[int64_t(i) * p.hdr_row + jj] = coef_base[int64_t(i) * p.coef_row + jj];
+        }
+    }
+}
+
+template <int NT, int PF, int VW, bool SH64>
+hipError_t launch_stream3(const MatmulParams &q, int row_tiles, int col_blocks, hipStream_t s) {
+    if (col_blocks % VW) return launch_stream3<NT, PF, 1, SH64>(q, row_tiles, col_blocks, s);
+    const int64_t total = int64_t(q.n_obj) * row_tiles * (col_blocks / VW);
+    if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gf_matmul_stream3_kernel<NT, PF, VW, SH64>), dim3(unsigned(total)), dim3(kThreads), 0, s, q,
+                       row_tiles, col_blocks / VW);
+    return hipGetLastError();
+}
+
+// Single-pass stream kernel form; RLNC_STREAM_FORM (A/B knob, read once): 0 = gf_matmul_stream_kernel<NT, 2>,
+// 8..13 = gf_matmul_stream3_kernel forms (profiles/r02_stream_ab.txt)
+int stream_form() {
+    static const int f = [] {
+        const char *e = getenv("RLNC_STREAM_FORM");
+        return e ? atoi(e) : RLNC_STREAM_FORM_DEFAULT;
+    }();
+    return f;
+}
+
 template <int NT>
 hipError_t launch_stream(const MatmulParams &p, int64_t full, hipStream_t s) {
     MatmulParams q = p;
     q.width = full;
     const int row_tiles = (p.n_out + NT - 1) / NT;
     const int col_blocks = int(full / kColBlock);
+    if (p.n_in <= kKC) {
+        switch (stream_form()) {
+            case 8: return launch_stream3<NT, 2, 1, true>(q, row_tiles, col_blocks, s);
+            case 9: return launch_stream3<NT, 2, 2, true>(q, row_tiles, col_blocks, s);
+            case 10: return launch_stream3<NT, 2, 2, false>(q, row_tiles, col_blocks, s);
+            case 11: return launch_stream3<NT, 1, 2, true>(q, row_tiles, col_blocks, s);
+            case 12: return launch_stream3<NT, 3, 1, true>(q, row_tiles, col_blocks, s);
+            case 13: return launch_stream3<NT, 2, 1, false>(q, row_tiles, col_blocks, s);
+            default: break;
+        }
+    }
     const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
     if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
 #ifndef RLNC_STREAM_PF

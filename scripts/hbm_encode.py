@@ -66,6 +66,12 @@ def main():
             o = 3
             want = np_matmul(co[o].cpu().numpy(), src[o, :, :4096].cpu().numpy(), MUL)
             ok = np.array_equal(out[o, :, k:k + 4096].cpu().numpy(), want)
+            if variant != 0:  # the whole output against the perm kernel (variant 0, independent code)
+                ref = torch.empty_like(out)
+                ctx.set_kernel_variant(0, 0)
+                batch.encode_batch(src, co, ref, ctx)
+                ctx.set_kernel_variant(variant, 0)
+                ok = ok and bool(torch.equal(ref, out))
             read = B * (k * L + n * k)
             write = B * n * (k + L)
             print(json.dumps({"n_coded": n, "variant": variant, "ms": round(ms, 4),

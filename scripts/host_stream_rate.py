@@ -6,7 +6,9 @@ object starts and ends in host memory and crosses PCIe through librlnc_hip's pip
     rlnc_encode_host_stream: source (host) → 64 coded pieces (host)
     rlnc_decode_host_stream: the first 32 coded pieces of each object (host, strided) → decoded rows (host)
 once with pinned host buffers (DMA straight from/to them) and once with pageable ones (staged through the
-library's pinned buffers by host threads).  Reports GiB/s in bench.py's counters, the PCIe bytes moved, the raw
+library's pinned buffers by host threads), each call after the other ("serial"); then, as an endpoint that both sends
+and receives does it, the encode of step i and the decode of step i-1 as two concurrent calls from two host threads
+on two contexts (pinned, "concurrent": two buffer sets, so both PCIe directions carry traffic at once).  Reports GiB/s in bench.py's counters, the PCIe bytes moved, the raw
 pinned copy rates of the box, and checks decoded == source for every object.
 """
 import argparse
@@ -70,6 +72,53 @@ def main():
                      "pcie_bytes_per_step": moved, "pcie_GBps_effective": round(moved / el / 1e9, 2),
                      "roundtrip_goodput_GiBps": round(B * k * L / el / 2**30, 3), "verified": bool(ok)}
         del src, co, pieces, dec
+    # concurrent: step i's encode (thread A, context A) beside step i-1's decode (thread B, context B); ctypes releases
+    # the GIL inside the library, so the two calls overlap on the device and on PCIe
+    import threading
+
+    ctx2 = rlnc_amd.Context(0)
+    buf = lambda shape: torch.empty(shape, dtype=torch.uint8, pin_memory=True)
+    src, co = buf((B, k, L)), buf((B, n, k))
+    src.numpy()[...] = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
+    co.numpy()[...] = rng.integers(0, 256, (B, n, k), dtype=np.uint8)
+    pieces = [buf((B, n, k + L)), buf((B, n, k + L))]
+    dec = buf((B, k, L))
+    ps = np.zeros((B, m), np.int32)
+    os_ = np.zeros(B, np.int32)
+    dl = np.zeros(B, np.uint64)
+    p = lambda t: C.c_void_p(t.data_ptr())
+    rcs = {}
+
+    def enc(i):
+        rcs["e"] = lib.rlnc_encode_host_stream(ctx.h, p(src), k, L, B, p(co), n, p(pieces[i % 2]), args.window)
+
+    def decd(i):
+        rcs["d"] = lib.rlnc_decode_host_stream(ctx2.h, p(pieces[(i - 1) % 2]), n * (k + L), k, L, m, B, p(dec),
+                                               ps.ctypes.data_as(C.POINTER(C.c_int32)),
+                                               os_.ctypes.data_as(C.POINTER(C.c_int32)),
+                                               dl.ctypes.data_as(C.POINTER(C.c_uint64)), args.window)
+
+    def cstep(i):
+        ts = [threading.Thread(target=enc, args=(i,))] + ([threading.Thread(target=decd, args=(i,))] if i else [])
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert all(v == 0 for v in rcs.values()), rcs
+
+    cstep(0)
+    cstep(1)  # warm-up: both contexts' pipeline buffers allocated
+    t0 = time.perf_counter()
+    for i in range(2, 2 + args.steps):
+        cstep(i)
+    el = (time.perf_counter() - t0) / args.steps
+    ok = all((ps[o] == 0).sum() < k or np.array_equal(dec.numpy()[o], src.numpy()[o]) for o in range(B))
+    moved = B * (k * L + n * k + n * (k + L) + m * (k + L) + k * L)
+    out["concurrent"] = {"value": round(bench.step_bytes(B, k, L, n) / el / 2**30, 2), "ms_per_step": round(el * 1e3, 2),
+                         "pcie_bytes_per_step": moved, "pcie_GBps_effective": round(moved / el / 1e9, 2),
+                         "roundtrip_goodput_GiBps": round(B * k * L / el / 2**30, 3), "verified": bool(ok),
+                         "how": "encode of step i and decode of step i-1 from two host threads on two contexts"}
+    del src, co, pieces, dec
     # raw pinned copy rates of this box
     big_h = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
     big_d = torch.empty(1 << 30, dtype=torch.uint8, device="cuda:0")
