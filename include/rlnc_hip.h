@@ -127,7 +127,9 @@ int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc);
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows);
 /* Where rlnc_decode_batch runs the coefficient elimination: 0 = auto (device when it fits LDS, default),
  * 1 = host threads, 2 = device, 3 = device with the clean-state steps on LDS instead of registers, 4 = device
- * with the clean-state steps on one wave's registers (2 spreads the initial clean run over 4 waves when k <= 64).
+ * with the clean-state steps on one wave's registers, 5 = device, blocked clean run (up to 16 pieces per step,
+ * 4 waves per object; k + m <= 256 -- what 0 and 2 use when it applies), 6 = device, the round-1 register path
+ * (initial clean run over 4 waves when k <= 64).
  * All are exact replicas; the switch exists for A/B tests. */
 int rlnc_set_decode_path(rlnc_context *ctx, int path);
 

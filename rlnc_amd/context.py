@@ -48,7 +48,8 @@ class Context:
 
     def set_decode_path(self, path: int = 0):
         """0 auto, 1 host elimination, 2 device elimination, 3 device with the clean state on LDS, 4 device on
-        one wave's registers (all exact; 2-4 exist for A/B)."""
+        one wave's registers, 5 device blocked clean run (what 0/2 use when k + m <= 256), 6 device, the round-1
+        multi-wave register path (all exact; 2-6 exist for A/B)."""
         check(self.lib.rlnc_set_decode_path(self.h, int(path)), self.lib)
 
     def set_kernel_variant(self, variant: int = 8, max_tile_rows: int = 0):

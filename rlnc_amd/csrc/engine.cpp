@@ -231,7 +231,7 @@ int rlnc_context_synchronize(rlnc_context *ctx) {
 }
 
 int rlnc_set_decode_path(rlnc_context *ctx, int path) {
-    CHECK_ARG(ctx != nullptr && path >= 0 && path <= 4);
+    CHECK_ARG(ctx != nullptr && path >= 0 && path <= 6);
     ctx->decode_path = path;
     return RLNC_OK;
 }
@@ -869,7 +869,7 @@ static int decode_eliminate_impl(rlnc_context *ctx, const uint8_t *pieces, size_
     rp.T_obj = int64_t(k * m);
     rp.status = pstat_dev;
     rp.rank = rank_dev;
-    rp.lds_only = ctx->decode_path == 3 ? 1 : ctx->decode_path == 4 ? 2 : 0;
+    rp.lds_only = ctx->decode_path == 3 ? 1 : ctx->decode_path == 4 ? 2 : ctx->decode_path == 5 ? 3 : ctx->decode_path == 6 ? 4 : 0;
     HIP_TRY(rlnc::launch_rref_batch(rp, ctx->stream));
     return RLNC_OK;
 }

@@ -74,7 +74,8 @@ struct RrefParams {
     int64_t T_obj;
     int32_t *status;
     int32_t *rank;
-    int lds_only;  // clean-state path (A/B, all exact): 0 registers, multi-wave when it fits; 1 LDS; 2 registers, one wave
+    int lds_only;  // clean-state path (A/B, all exact): 0 auto (blocked clean run when k + m <= 256, else 4);
+                   // 1 LDS; 2 registers, one wave; 3 blocked clean run (gf_rref_block_kernel); 4 registers, multi-wave
 };
 constexpr size_t kRrefMaxLds = 160 * 1024;
 size_t rref_lds_bytes(int k, int m);

@@ -146,7 +146,21 @@ __device__ __forceinline__ void row_muladd(const Mat &M, const uint32_t *tab, in
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
+// WG: a workgroup barrier; else the code runs in one wave only (the other waves of the workgroup are elsewhere and
+// must not be waited for): a compiler fence suffices, a wave's LDS operations execute in issue order
+template <bool WG>
+__device__ __forceinline__ void rsync() {
+    if constexpr (WG) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 // DecoderMatrix::rref — decoder_matrix.rs:99-244, verbatim.  Returns the new row count.
+template <bool WG = true>
 __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
     const int lane = threadIdx.x;
     // clean_forward :120-166 (boundary = min(rows, cols) = rows, since rows <= k < cols)
@@ -165,7 +179,7 @@ __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
                 M.w[i * M.D + w] = M.w[found * M.D + w];
                 M.w[found * M.D + w] = a;
             }
-            __syncthreads();
+            rsync<WG>();
             piv = M.at(i, i);
         }
         const uint32_t inv = gfinv(tab, piv);
@@ -179,7 +193,7 @@ __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
                 row_muladd(M, tab, jj, i, q, i);
             }
         }
-        __syncthreads();
+        rsync<WG>();
     }
     // clean_backward :171-215
     for (int i = R - 1; i >= 0; --i) {
@@ -196,7 +210,7 @@ __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
                 row_muladd(M, tab, jj, i, q, i);
             }
         }
-        __syncthreads();
+        rsync<WG>();
         if (piv != 1) {  // :200-211
             for (int w = lane; w < M.D; w += 64) {
                 const uint32_t mask = from_mask(w, i + 1);
@@ -205,9 +219,9 @@ __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
                     M.w[i * M.D + w] = (x & ~mask) | (mul4(tab, inv, x) & mask);
                 }
             }
-            __syncthreads();
+            rsync<WG>();
             if (lane == 0) M.b[i * M.S + i] = 1;
-            __syncthreads();
+            rsync<WG>();
         }
     }
     // remove_zero_rows :222-244 (zero test on the first k columns), order preserved
@@ -226,12 +240,12 @@ __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
             const int src = g + q;
             if (src != dst) {
                 for (int w = lane; w < M.D; w += 64) M.w[dst * M.D + w] = M.w[src * M.D + w];
-                __syncthreads();
+                rsync<WG>();
             }
             ++dst;
         }
     }
-    __syncthreads();
+    rsync<WG>();
     return dst;
 }
 
@@ -816,6 +830,493 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, in
 #endif
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// Blocked clean run (path 5, default when k + m <= 256): while rows 0..r-1 are a clean RREF, the next b <= B
+// pieces are appended in one block instead of one at a time:
+//   1. X_t = init_t ^ Σ_{i<r} P_t[i]·R_i for t < b — the forward pass of every piece of the block against the r
+//      clean rows (the quotients are the original coefficients, file header), summed over (wave, lane group)
+//      stripes of i and met in LDS by ds_xor;
+//   2. the b rows among themselves, exactly as the one-piece clean step would take them in order: y_t ^=
+//      Σ_{s<t} X_t[r+s]·y_s, pivot y_t[r+t], normalise from r+t+1 by its inverse, eliminate column r+t from the
+//      y_s (s < t) — every wave does this redundantly in registers (lane = dword), so no wave waits for another;
+//   3. R_j ^= Σ_{t<c} R_j[r+t]·y_t for every row j < r (rows striped over waves and lane groups), y_t appended as
+//      rows r..r+c-1.
+// Same state as c one-piece steps: the clean RREF with pivots 0..r+c-1 of span(R, P_0..P_{c-1}) is unique, and y_t
+// is the unique vector of P_t + span(committed rows) that is zero in columns 0..r+t-1, which is what the forward
+// pass of the one-piece step computes — so pivot tests, normalised rows and statuses are identical.  A zero pivot
+// at t ends the block after c = t pieces: piece t's reduced row y_t is then exactly clean_append's row (kept, the
+// clean state ends, iff a coefficient byte is nonzero).  Outside the clean state every piece runs the reference
+// algorithm verbatim (generic_rref) in wave 0 while the other waves wait at the next workgroup barrier, and the
+// blocked run resumes once is_clean holds again.
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint32_t byte_of(uint32_t v, int lane_dw, int b) {
+    return (uint32_t(__builtin_amdgcn_readlane(int(v), lane_dw)) >> (8 * b)) & 0xFFu;
+}
+
+
+// ---- the non-clean step of the blocked kernel (rows 0..cp-1 a clean prefix, rows cp..R-1 dirty) --------------
+// Clean prefix: for i < cp, M[i][i] = 1 and column i is zero in every other row < cp.  The reference's rref
+// (decoder_matrix.rs:99-244) on such a matrix splits exactly: its forward steps i < cp only reduce the dirty
+// rows against the prefix rows (pivot 1, quotient = the dirty row's original byte i, since a prefix row is zero in
+// every other prefix column) and never swap; its forward steps i >= cp touch dirty rows only; its backward steps
+// i >= cp eliminate column i from every row above (prefix rows included), and its backward steps i < cp do
+// nothing (column i is zero above row i, the pivot is 1); remove_zero_rows can only drop dirty rows.
+
+// forward steps i in [r0, R) of clean_forward (:120-166), verbatim, on rows >= r0 (one wave)
+__device__ void forward_range(const Mat &M, const uint32_t *tab, int r0, int R) {
+    const int lane = threadIdx.x & 63;
+    for (int i = r0; i < R; ++i) {
+        uint32_t piv = M.at(i, i);
+        if (piv == 0) {
+            int found = -1;
+            for (int g = i + 1; g < R && found < 0; g += 64) {
+                const int j = g + lane;
+                const uint64_t b = ballot(j < R && M.at(j, i) != 0);
+                if (b) found = g + __ffsll((unsigned long long)b) - 1;
+            }
+            if (found < 0) continue;
+            for (int w = lane; w < M.D; w += 64) {  // swap_rows :69-90
+                const uint32_t a = M.w[i * M.D + w];
+                M.w[i * M.D + w] = M.w[found * M.D + w];
+                M.w[found * M.D + w] = a;
+            }
+            rsync<false>();
+            piv = M.at(i, i);
+        }
+        const uint32_t inv = gfinv(tab, piv);
+        for (int g = i + 1; g < R; g += 64) {
+            const int j = g + lane;
+            uint64_t b = ballot(j < R && M.at(j, i) != 0);
+            while (b) {
+                const int jj = g + __ffsll((unsigned long long)b) - 1;
+                b &= b - 1;
+                const uint32_t q = gfmul(tab, M.at(jj, i), inv);  // :148
+                for (int w = lane; w < M.D; w += 64) {
+                    const uint32_t mask = from_mask(w, i);
+                    if (mask) M.w[jj * M.D + w] ^= mul4(tab, q, M.w[i * M.D + w]) & mask;
+                }
+            }
+        }
+        rsync<false>();
+    }
+}
+
+// remove_zero_rows (:222-244) over rows [r0, R) (zero test on the first k columns, order preserved); one wave
+__device__ int remove_zero_range(const Mat &M, int r0, int R, int k) {
+    const int lane = threadIdx.x & 63;
+    int dst = r0;
+    for (int g = r0; g < R; g += 64) {
+        const int r = g + lane;
+        bool nz = false;
+        if (r < R)
+            for (int c4 = 0; 4 * c4 < k && !nz; ++c4) {
+                const uint32_t x = M.w[r * M.D + c4];
+                nz = (4 * c4 + 4 <= k ? x : (x & (0xFFFFFFFFu >> (8 * (4 * c4 + 4 - k))))) != 0;
+            }
+        const uint64_t keep = ballot(nz);
+        for (int q = 0; q < 64 && g + q < R; ++q) {
+            if (!((keep >> q) & 1ull)) continue;
+            const int src = g + q;
+            if (src != dst) {
+                for (int w = lane; w < M.D; w += 64) M.w[dst * M.D + w] = M.w[src * M.D + w];
+                rsync<false>();
+            }
+            ++dst;
+        }
+    }
+    rsync<false>();
+    return dst;
+}
+
+// extends the clean prefix from cp while row cp has M[cp][cp] = 1, zeros in columns < cp, and column cp is zero in
+// every row above it; one wave
+__device__ int extend_prefix(const Mat &M, int cp, int R) {
+    const int lane = threadIdx.x & 63;
+    while (cp < R) {
+        const int c = cp;
+        bool bad = false;
+        for (int j = lane; j < c; j += 64) bad |= M.at(j, c) != 0;         // column c above row c
+        for (int w = lane; 4 * w < c; w += 64) {                            // row c left of column c
+            const uint32_t x = M.w[c * M.D + w];
+            bad |= (4 * w + 4 <= c ? x : (x & (0xFFFFFFFFu >> (8 * (4 * w + 4 - c))))) != 0;
+        }
+        if (ballot(bad) != 0 || M.at(c, c) != 1) break;
+        ++cp;
+    }
+    return cp;
+}
+
+struct Sel1 {  // v_perm selectors of one dword: bits 0-2, 3-5, 6-7 of every byte
+    uint32_t s0, s1, s2;
+};
+
+template <int NW, int B>
+__global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
+    extern __shared__ uint32_t lds[];
+    uint32_t *tab = lds;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int o = blockIdx.x;
+    const int k = p.k, m = p.m;
+    const int kH = (k + 3) & ~3;  // staged header stride (dword-aligned coefficient groups, zero padded)
+    Mat M;
+    M.D = rref_row_dwords(k, m);  // <= 64 here
+    M.S = 4 * M.D;
+    M.w = lds + kTabEntries * kTabDw;
+    M.b = reinterpret_cast<uint8_t *>(M.w);
+    const int D = M.D;
+    const int G = 64 / D;                     // lane groups per wave (one matrix row each)
+    const int w = lane % D, g = lane / D;     // this lane's dword and group
+    const int NS = NW * G, sid = wave * G + g;  // stripes
+    int32_t *St = reinterpret_cast<int32_t *>(M.b + size_t(k + 1) * M.S);
+    uint8_t *H = reinterpret_cast<uint8_t *>(St + ((m + 3) & ~3));
+    uint32_t *X = reinterpret_cast<uint32_t *>(H + ((size_t(m) * kH + 15) & ~size_t(15)));  // B x D dwords
+    int *flag = reinterpret_cast<int *>(X + B * D);
+#ifdef RLNC_RREF_PROFILE  // diagnostic build: statuses 0..7 of each object become phase cycle counts (wave 0)
+    uint64_t bprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t bt = __builtin_amdgcn_s_memtime();
+    const uint64_t bt0 = bt;
+#define BPROF(i)                                          \
+    do {                                                  \
+        const uint64_t _t = __builtin_amdgcn_s_memtime(); \
+        bprof[i] += _t - bt;                              \
+        bt = _t;                                          \
+    } while (0)
+#else
+#define BPROF(i) \
+    do {         \
+    } while (0)
+#endif
+
+    {  // the multiplier tables: all loads in flight at once
+        constexpr int kPer = kTabEntries * kTabDw / 4 / (64 * NW);
+        const uint4 *src = reinterpret_cast<const uint4 *>(kRrefTable.v);
+        uint4 *dst = reinterpret_cast<uint4 *>(tab);
+        uint4 t4[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) t4[u] = src[tid + 64 * NW * u];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) dst[tid + 64 * NW * u] = t4[u];
+    }
+    const uint8_t *base = p.pieces + int64_t(o) * p.obj_stride;
+    for (int e0 = 0; e0 < m * kH; e0 += 64 * NW * 16) {  // headers, 16 byte loads in flight per thread
+        uint8_t hb[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = e0 + tid + 64 * NW * u;
+            const int pc = e / kH, c = e % kH;
+            hb[u] = (e < m * kH && c < k) ? base[int64_t(pc) * p.piece_stride + c] : uint8_t(0);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            if (e0 + tid + 64 * NW * u < m * kH) H[e0 + tid + 64 * NW * u] = hb[u];
+    }
+    for (int e = tid; e < (k + 1) * D; e += 64 * NW) M.w[e] = 0;
+    __syncthreads();
+
+    BPROF(0);  // setup: tables, headers, zeroed matrix
+    uint32_t cm = 0;  // coefficient bytes (< k) of this lane's dword
+    if (4 * w < k) cm = 4 * w + 4 <= k ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (8 * (4 * w + 4 - k)));
+    int rows = 0, pc = 0, cp = 0;  // cp: clean prefix (== rows in the clean state)
+    bool clean = true;
+    while (pc < m) {
+        if (rows == k) {  // decoder.rs:97-99
+            for (int q = pc + tid; q < m; q += 64 * NW) St[q] = RLNC_ERR_RECEIVED_ALL_PIECES;
+            break;
+        }
+        if (!clean) {
+            const int r0 = cp, R = rows;  // rows r0..R-1 dirty; this piece becomes row R
+            if (R + 1 - r0 > B) {  // many dirty rows: the reference verbatim, wave 0
+                if (wave == 0) {
+                    for (int c = lane; c < M.S; c += 64)
+                        M.b[R * M.S + c] = c < k ? H[pc * kH + c] : uint8_t(c == k + pc);
+                    rsync<false>();
+                    const int r2 = generic_rref<false>(M, tab, R + 1, k);
+                    const int cp2 = extend_prefix(M, r0, r2);
+                    if (lane == 0) {
+                        St[pc] = r2 == R ? RLNC_ERR_PIECE_NOT_USEFUL : RLNC_OK;  // decoder.rs:112-117
+                        flag[0] = r2;
+                        flag[1] = cp2;
+                    }
+                }
+            } else {
+                const int nb = R + 1 - r0;  // dirty rows including the new one
+                for (int c = tid; c < M.S; c += 64 * NW) M.b[R * M.S + c] = c < k ? H[pc * kH + c] : uint8_t(c == k + pc);
+                for (int e = tid; e < B * D; e += 64 * NW) X[e] = 0;
+                __syncthreads();
+                // forward steps i < r0: the dirty rows reduced against the prefix (stripes of i, met by ds_xor)
+                {
+                    uint32_t acc[B];
+#pragma unroll
+                    for (int t = 0; t < B; ++t) acc[t] = 0;
+                    for (int i0 = 4 * sid; i0 < r0; i0 += 4 * NS) {
+                        uint32_t x[4];
+#pragma unroll
+                        for (int ii = 0; ii < 4; ++ii) x[ii] = i0 + ii < r0 ? M.w[(i0 + ii) * D + w] : 0u;
+                        uint32_t q4[B];
+#pragma unroll
+                        for (int t = 0; t < B; ++t) {
+                            const uint32_t v = M.w[min(r0 + t, R) * D + (i0 >> 2)];
+                            q4[t] = t < nb ? v : 0u;
+                        }
+#pragma unroll
+                        for (int t = 0; t < B; ++t)
+#pragma unroll
+                            for (int ii = 0; ii < 4; ++ii) acc[t] ^= mul4(tab, (q4[t] >> (8 * ii)) & 0xFFu, x[ii]);
+                    }
+#pragma unroll
+                    for (int t = 0; t < B; ++t) {
+                        if (t < nb) {
+                            uint32_t a = acc[t];
+                            for (int sh = D; sh < 64; sh <<= 1) a ^= __shfl_xor(a, sh);
+                            if (g == 0 && a) atomicXor(&X[t * D + w], a);
+                        }
+                    }
+                }
+                __syncthreads();
+                for (int e = tid; e < nb * D; e += 64 * NW) M.w[r0 * D + e] ^= X[e];
+                __syncthreads();
+                // forward steps i >= r0, verbatim on the dirty rows
+                if (wave == 0) forward_range(M, tab, r0, R + 1);
+                __syncthreads();
+                // backward steps i = R .. r0 (:171-215): column i out of every row above (stripes), then row i
+                // normalised from column i+1
+                for (int i = R; i >= r0; --i) {
+                    const uint32_t piv = M.at(i, i);
+                    if (piv == 0) continue;  // every wave reads the same byte (no write since the last barrier)
+                    const uint32_t xi = M.w[i * D + w];
+                    const uint32_t nr = mul4(tab, 256 + piv, xi);  // row i · piv^-1: (q·piv^-1)·x = q·(piv^-1·x)
+                    const uint32_t mi = from_mask(w, i);
+                    for (int j = sid; j < i; j += NS) {
+                        const uint32_t q = M.at(j, i);
+                        if (q) M.w[j * D + w] ^= mul4(tab, q, nr) & mi;
+                    }
+                    __syncthreads();
+                    if (piv != 1) {
+                        if (tid < D) {
+                            const uint32_t mask = from_mask(w, i + 1);
+                            uint32_t v = (xi & ~mask) | (nr & mask);
+                            if (w == (i >> 2)) v = (v & ~(0xFFu << (8 * (i & 3)))) | (1u << (8 * (i & 3)));
+                            M.w[i * D + w] = v;
+                        }
+                        __syncthreads();
+                    }
+                }
+                if (wave == 0) {
+                    const int r2 = remove_zero_range(M, r0, R + 1, k);
+                    const int cp2 = extend_prefix(M, r0, r2);
+                    if (lane == 0) {
+                        St[pc] = r2 == R ? RLNC_ERR_PIECE_NOT_USEFUL : RLNC_OK;  // decoder.rs:112-117
+                        flag[0] = r2;
+                        flag[1] = cp2;
+                    }
+                }
+            }
+            __syncthreads();
+            rows = flag[0];
+            cp = flag[1];
+            clean = cp == rows;
+            ++pc;
+            __syncthreads();
+            BPROF(5);  // one piece outside the clean state
+            continue;
+        }
+        const int r = rows;
+        const int b = min(B, min(m - pc, k - r));
+        // 1. X_t = init_t ^ Σ_{i<r} P_t[i]·R_i
+        for (int e = tid; e < B * D; e += 64 * NW) {
+            const int t = e / D, ww = e % D;
+            uint32_t x = 0;
+            if (t < b) {
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                    const int c = 4 * ww + bb;
+                    x |= (c < k ? uint32_t(H[(pc + t) * kH + c]) : uint32_t(c == k + pc + t)) << (8 * bb);
+                }
+            }
+            X[e] = x;
+        }
+        __syncthreads();
+        if (r > 0) {
+            uint32_t acc[B];
+#pragma unroll
+            for (int t = 0; t < B; ++t) acc[t] = 0;
+            const uint32_t *H32 = reinterpret_cast<const uint32_t *>(H);
+            for (int i0 = 4 * sid; i0 < r; i0 += 4 * NS) {
+                uint32_t x[4];
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii) x[ii] = i0 + ii < r ? M.w[(i0 + ii) * D + w] : 0u;  // rows >= r: 0
+                // the 4 coefficients P_t[i0..i0+3] of every piece of the block (0 past the block: zero products),
+                // all read before any table read, and no branch on t: the reads of a chunk overlap
+                uint32_t q4[B];
+#pragma unroll
+                for (int t = 0; t < B; ++t) {
+                    const uint32_t v = H32[(min(pc + t, m - 1) * kH + i0) >> 2];
+                    q4[t] = t < b ? v : 0u;
+                }
+                Sel1 sl[4];
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii) {
+                    sl[ii].s0 = x[ii] & 0x07070707u;
+                    sl[ii].s1 = (x[ii] >> 3) & 0x07070707u;
+                    sl[ii].s2 = (x[ii] >> 6) & 0x03030303u;
+                }
+#pragma unroll
+                for (int t = 0; t < B; ++t) {
+#pragma unroll
+                    for (int ii = 0; ii < 4; ++ii) {
+                        const uint32_t q = (q4[t] >> (8 * ii)) & 0xFFu;
+                        const uint4 t4 = *reinterpret_cast<const uint4 *>(tab + q * kTabDw);
+                        const uint32_t t2 = tab[q * kTabDw + 4];
+                        acc[t] = xor3(acc[t], __builtin_amdgcn_perm(t4.y, t4.x, sl[ii].s0),
+                                      xor3(__builtin_amdgcn_perm(t4.w, t4.z, sl[ii].s1), __builtin_amdgcn_perm(t2, t2, sl[ii].s2), 0u));
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < B; ++t) {
+                if (t < b) {
+                    uint32_t a = acc[t];
+                    for (int sh = D; sh < 64; sh <<= 1) a ^= __shfl_xor(a, sh);
+                    if (g == 0 && a) atomicXor(&X[t * D + w], a);
+                }
+            }
+            __syncthreads();
+        }
+        BPROF(1);  // step 1 (with the block's initial rows)
+        // 2. the block's rows among themselves (every wave, registers; lane groups hold identical copies).  No
+        // branch inside a piece's forward or backward products: their table reads are issued together.
+        uint32_t y[B];
+#pragma unroll
+        for (int t = 0; t < B; ++t) y[t] = t < b ? X[t * D + w] : 0u;
+        int c = b;
+#pragma unroll
+        for (int t = 0; t < B; ++t) {
+            if (t < c) {
+                // forward: quotients are the block-reduced row's bytes r+s (s < t), read before any update
+                uint32_t acc = y[t];
+                {
+                    uint4 f4[B];
+                    uint32_t f2[B];
+#pragma unroll
+                    for (int s2 = 0; s2 < t; ++s2) {
+                        const uint32_t q = byte_of(y[t], (r + s2) >> 2, (r + s2) & 3);
+                        f4[s2] = *reinterpret_cast<const uint4 *>(tab + q * kTabDw);
+                        f2[s2] = tab[q * kTabDw + 4];
+                    }
+#pragma unroll
+                    for (int s2 = 0; s2 < t; ++s2) acc ^= mul4t(f4[s2], f2[s2], y[s2]);
+                }
+                y[t] = acc;
+                const uint32_t piv = byte_of(y[t], (r + t) >> 2, (r + t) & 3);
+                if (piv == 0) {
+                    c = t;
+                } else {
+                    const uint32_t mask = from_mask(w, r + t + 1);  // normalise from column r+t+1 (:200-211)
+                    y[t] = (y[t] & ~mask) | (mul4(tab, 256 + piv, y[t]) & mask);
+                    if (w == ((r + t) >> 2)) y[t] = (y[t] & ~(0xFFu << (8 * ((r + t) & 3)))) | (1u << (8 * ((r + t) & 3)));
+                    // backward inside the block: y_s ^= y_s[r+t]·y_t (s < t), y_t's selectors shared
+                    const uint32_t e0 = y[t] & 0x07070707u, e1 = (y[t] >> 3) & 0x07070707u, e2 = (y[t] >> 6) & 0x03030303u;
+                    uint4 b4[B];
+                    uint32_t b2[B];
+#pragma unroll
+                    for (int s2 = 0; s2 < t; ++s2) {
+                        const uint32_t qb = byte_of(y[s2], (r + t) >> 2, (r + t) & 3);
+                        b4[s2] = *reinterpret_cast<const uint4 *>(tab + qb * kTabDw);
+                        b2[s2] = tab[qb * kTabDw + 4];
+                    }
+#pragma unroll
+                    for (int s2 = 0; s2 < t; ++s2)
+                        y[s2] = xor3(y[s2], __builtin_amdgcn_perm(b4[s2].y, b4[s2].x, e0),
+                                     xor3(__builtin_amdgcn_perm(b4[s2].w, b4[s2].z, e1), __builtin_amdgcn_perm(b2[s2], b2[s2], e2), 0u));
+                }
+            }
+        }
+        BPROF(2);
+        // 3. rows j < r: R_j ^= Σ_{t<c} R_j[r+t]·y_t; then y_t become rows r..r+c-1
+        if (c > 0) {
+            Sel1 ys[B];
+#pragma unroll
+            for (int t = 0; t < B; ++t) {
+                ys[t].s0 = y[t] & 0x07070707u;
+                ys[t].s1 = (y[t] >> 3) & 0x07070707u;
+                ys[t].s2 = (y[t] >> 6) & 0x03030303u;
+            }
+            const int d0 = r >> 2, sh = r & 3;
+            for (int j = sid; j < r; j += NS) {
+                uint32_t cw[(B + 3) / 4 + 1];  // the dwords holding bytes r .. r+B-1 of row j
+#pragma unroll
+                for (int u = 0; u < (B + 3) / 4 + 1; ++u) cw[u] = d0 + u < D ? M.w[j * D + d0 + u] : 0u;
+                uint32_t qw[(B + 3) / 4];  // bytes r.. aligned to dword boundaries
+#pragma unroll
+                for (int u = 0; u < (B + 3) / 4; ++u) qw[u] = __builtin_amdgcn_alignbyte(cw[u + 1], cw[u], sh);
+                uint32_t xj = M.w[j * D + w];
+#pragma unroll
+                for (int t = 0; t < B; ++t) {  // no branch: pieces past c multiply by 0
+                    const uint32_t qq = t < c ? (qw[t >> 2] >> (8 * (t & 3))) & 0xFFu : 0u;
+                    const uint4 t4 = *reinterpret_cast<const uint4 *>(tab + qq * kTabDw);
+                    const uint32_t t2 = tab[qq * kTabDw + 4];
+                    xj = xor3(xj, __builtin_amdgcn_perm(t4.y, t4.x, ys[t].s0),
+                              xor3(__builtin_amdgcn_perm(t4.w, t4.z, ys[t].s1), __builtin_amdgcn_perm(t2, t2, ys[t].s2), 0u));
+                }
+                M.w[j * D + w] = xj;
+            }
+            if (wave == 0 && g == 0) {
+#pragma unroll
+                for (int t = 0; t < B; ++t)
+                    if (t < c) M.w[(r + t) * D + w] = y[t];
+            }
+            if (tid < c) St[pc + tid] = RLNC_OK;
+        }
+        BPROF(3);
+        rows = r + c;
+        pc += c;
+        if (c < b) {  // piece pc: zero pivot after its forward pass; its reduced row is y[c]
+            uint32_t yc = 0;
+#pragma unroll
+            for (int t = 0; t < B; ++t)
+                if (t == c) yc = y[t];
+            const bool keep = __ballot(g == 0 && (yc & cm) != 0) != 0;  // remove_zero_rows (:222-244)
+            if (keep && wave == 0 && g == 0) M.w[rows * D + w] = yc;
+            if (tid == 0) St[pc] = keep ? RLNC_OK : RLNC_ERR_PIECE_NOT_USEFUL;
+            if (keep) {
+                cp = rows;
+                ++rows;
+                clean = false;
+            }
+            ++pc;
+        }
+        __syncthreads();
+        BPROF(4);  // zero-pivot piece + the block's closing barrier
+    }
+    __syncthreads();
+#ifdef RLNC_RREF_PROFILE
+    bprof[6] = __builtin_amdgcn_s_memtime() - bt0;
+    if (tid == 0)
+        for (int i = 0; i < 8 && i < m; ++i) St[i] = int32_t(bprof[i]);
+    __syncthreads();
+#endif
+    for (int q = tid; q < m; q += 64 * NW) p.status[int64_t(o) * m + q] = St[q];
+    if (tid == 0) p.rank[o] = rows;
+    uint8_t *T = p.T + int64_t(o) * p.T_obj;
+    for (int e = tid; e < k * m; e += 64 * NW) {
+        const int rr = e / m, s2 = e % m;
+        T[e] = rr < rows ? M.b[rr * M.S + k + s2] : uint8_t(0);
+    }
+}
+
+constexpr int kBlkNW = 4, kBlkB = 16;
+
+size_t rref_block_lds_bytes(int k, int m) {
+    const int D = rref_row_dwords(k, m);
+    return size_t(kTabEntries) * kTabDw * 4 + size_t(k + 1) * 4 * D + 4 * ((size_t(m) + 3) & ~size_t(3)) +
+           ((size_t(m) * ((k + 3) & ~3) + 15) & ~size_t(15)) + size_t(kBlkB) * D * 4 + 16;
+}
+
 }  // namespace
 
 size_t rref_lds_bytes(int k, int m) {
@@ -828,6 +1329,28 @@ static size_t rref_lds_bytes_staged(int k, int m) {
 
 hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     if (p.n_obj <= 0) return hipSuccess;
+    // the blocked clean run (4 waves per object, the default) when the row fits one wave (k + m <= 256)
+    if ((p.lds_only == 0 || p.lds_only == 3) && rref_row_dwords(p.k, p.m) <= 64 &&
+        rref_block_lds_bytes(p.k, p.m) <= kRrefMaxLds) {
+        static std::mutex mu;
+        static bool attr_set[64] = {};
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+        {
+            std::lock_guard<std::mutex> lock(mu);
+            if (!attr_set[dev]) {
+                e = hipFuncSetAttribute(reinterpret_cast<const void *>(&gf_rref_block_kernel<kBlkNW, kBlkB>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(kRrefMaxLds));
+                if (e != hipSuccess) return e;
+                attr_set[dev] = true;
+            }
+        }
+        hipLaunchKernelGGL((gf_rref_block_kernel<kBlkNW, kBlkB>), dim3(p.n_obj), dim3(64 * kBlkNW),
+                           rref_block_lds_bytes(p.k, p.m), s, p);
+        return hipGetLastError();
+    }
     size_t lds = rref_lds_bytes(p.k, p.m);
     if (lds > kRrefMaxLds) return hipErrorInvalidValue;
     const int hdr_lds = rref_lds_bytes_staged(p.k, p.m) <= kRrefMaxLds ? 1 : 0;
@@ -838,7 +1361,7 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     auto kern = &gf_rref_batch_kernel<0, 1, 1>;
     int threads = 64;
     if (p.lds_only != 1 && hdr_lds) {  // the register paths read the staged headers
-        const bool mw = p.lds_only == 0;
+        const bool mw = p.lds_only == 0 || p.lds_only == 4;
         if (D <= 16 && p.k <= 32) {
             kern = mw ? &gf_rref_batch_kernel<4, 8, 4, 4, 2> : &gf_rref_batch_kernel<4, 8, 1>;
         } else if (D <= 32 && p.k <= 64) {

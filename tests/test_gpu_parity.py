@@ -309,7 +309,7 @@ def test_golden_decode_object_api(ctx, golden):
             assert e.name == v["final_status"], v["name"]
 
 
-@pytest.mark.parametrize("path", [1, 2, 3, 4])
+@pytest.mark.parametrize("path", [1, 2, 3, 4, 5, 6])
 def test_golden_decode_batch(ctx, golden, path):
     from rlnc_amd import batch
 
@@ -349,7 +349,7 @@ def _sequences(rng, nobj, k, m, L, sparsity, dep_frac):
     return seqs
 
 
-@pytest.mark.parametrize("path", [1, 2, 3, 4])
+@pytest.mark.parametrize("path", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("k,m,L,sparsity,dep", [(32, 32, 40, 0.0, 0.0), (64, 64, 24, 0.0, 0.1), (128, 128, 20, 0.0, 0.0),
                                                 (100, 120, 9, 0.0, 0.1), (120, 128, 16, 0.9, 0.02),
                                                 (48, 56, 10, 0.4, 0.1), (64, 70, 9, 0.85, 0.05), (8, 14, 5, 0.7, 0.1), (8, 12, 33, 0.9, 0.0), (32, 40, 64, 0.0, 0.2),
@@ -382,6 +382,33 @@ def test_decode_batch_vs_oracle_sequences(ctx, path, k, m, L, sparsity, dep):
         assert S[ost[o]] == S[st], o
         if st == 0:
             assert int(dl[o]) == data.size
+
+
+@pytest.mark.parametrize("k,m,sparsity,dep", [(32, 48, 0.5, 0.05), (64, 64, 0.3, 0.02), (16, 40, 0.6, 0.1),
+                                               (128, 128, 0.05, 0.0), (48, 64, 0.8, 0.0), (96, 100, 0.2, 0.05)])
+def test_decode_blocked_path_stress(ctx, k, m, sparsity, dep):
+    """The blocked elimination (path 5) against the oracle on 64 objects per shape: sparse coefficients drive the
+    matrix in and out of the clean state (zero pivots, kept dirty rows, prefix re-extension, the many-dirty-rows
+    fallback), dependent pieces hit PieceNotUseful; statuses, rank and payload rows must all match."""
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(5000 + k * 7 + m)
+    nobj, L = 64, 8
+    seqs = _sequences(rng, nobj, k, m, L, sparsity, dep)
+    decoded = dev(np.zeros((nobj, k, L), np.uint8))
+    ctx.set_decode_path(5)
+    try:
+        pst, ost, dl = batch.decode_batch(dev(seqs), k, decoded, ctx)
+    finally:
+        ctx.set_decode_path(0)
+    got = host(decoded)
+    for o in range(nobj):
+        od = OracleDecoder(L, k)
+        want = [S[od.decode(p)] for p in seqs[o]]
+        assert [S[x] for x in pst[o]] == want, (o, [S[x] for x in pst[o]], want)
+        pay = od.padded_payload()
+        assert np.array_equal(got[o, : pay.shape[0]], pay), o
+        assert not got[o, pay.shape[0]:].any()
 
 
 def test_decode_batch_device_async_outputs(ctx, orc):
