@@ -124,7 +124,7 @@ struct rlnc_context {
     int max_tile_rows = 0;
     int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination,
                           // 3 device elimination with the clean state on LDS, 4 ... on one wave's
-                          // registers (A/B)
+                          // registers, 5 blocked clean run, 6 round-1 multi-wave registers (A/B)
     // workspaces of the stream-ordered batch / _device API (one caller thread per context at a time)
     DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len, ws_pstat, ws_rank, ws_idx;
     PinBuf pin_a, pin_b, pin_c;

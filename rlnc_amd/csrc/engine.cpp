@@ -14,6 +14,7 @@
 #include <memory>
 #include <new>
 #include <string>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -907,6 +908,9 @@ static int decode_batch_device_impl(rlnc_context *ctx, const uint8_t *pieces, si
     int st;
     if ((st = ctx->grow(ctx->ws_coef, nobj * k * m))) return st;
     uint8_t *T = ctx->ws_coef.as<uint8_t>();
+    // (Eliminating the later objects on a second stream beside the first objects' T x data product measured slower:
+    // 8.3-8.6 ms against 7.99 for configs[4]'s 512 objects -- the concurrent elimination slows the product more
+    // than it hides; profiles/r02_decode_pipeline_ab.txt.)
     if ((st = decode_eliminate_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, pstat_dev, rank_dev))) return st;
     return decode_apply_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, rank_dev, decoded, ostat_dev, len_dev);
 }

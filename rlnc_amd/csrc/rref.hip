@@ -23,6 +23,7 @@
 // then never waits on HBM.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 
 #include "../../include/rlnc_hip.h"
@@ -1165,13 +1166,30 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
                     sl[ii].s1 = (x[ii] >> 3) & 0x07070707u;
                     sl[ii].s2 = (x[ii] >> 6) & 0x03030303u;
                 }
+                // the tables of piece t (its 4 coefficients), double-buffered: piece t+1's 8 LDS reads are in
+                // flight while piece t's products run
+                uint4 ta[2][4];
+                uint32_t tb[2][4];
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii) {
+                    const uint32_t q = (q4[0] >> (8 * ii)) & 0xFFu;
+                    ta[0][ii] = *reinterpret_cast<const uint4 *>(tab + q * kTabDw);
+                    tb[0][ii] = tab[q * kTabDw + 4];
+                }
 #pragma unroll
                 for (int t = 0; t < B; ++t) {
+                    if (t + 1 < B) {
+#pragma unroll
+                        for (int ii = 0; ii < 4; ++ii) {
+                            const uint32_t q = (q4[t + 1] >> (8 * ii)) & 0xFFu;
+                            ta[(t + 1) & 1][ii] = *reinterpret_cast<const uint4 *>(tab + q * kTabDw);
+                            tb[(t + 1) & 1][ii] = tab[q * kTabDw + 4];
+                        }
+                    }
 #pragma unroll
                     for (int ii = 0; ii < 4; ++ii) {
-                        const uint32_t q = (q4[t] >> (8 * ii)) & 0xFFu;
-                        const uint4 t4 = *reinterpret_cast<const uint4 *>(tab + q * kTabDw);
-                        const uint32_t t2 = tab[q * kTabDw + 4];
+                        const uint4 t4 = ta[t & 1][ii];
+                        const uint32_t t2 = tb[t & 1][ii];
                         acc[t] = xor3(acc[t], __builtin_amdgcn_perm(t4.y, t4.x, sl[ii].s0),
                                       xor3(__builtin_amdgcn_perm(t4.w, t4.z, sl[ii].s1), __builtin_amdgcn_perm(t2, t2, sl[ii].s2), 0u));
                     }
@@ -1191,9 +1209,9 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
         // 2. the block's rows among themselves (every wave, registers; lane groups hold identical copies).  No
         // branch inside a piece's forward or backward products: their table reads are issued together.
         uint32_t y[B];
+        int c = b;
 #pragma unroll
         for (int t = 0; t < B; ++t) y[t] = t < b ? X[t * D + w] : 0u;
-        int c = b;
 #pragma unroll
         for (int t = 0; t < B; ++t) {
             if (t < c) {
@@ -1247,23 +1265,38 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
                 ys[t].s2 = (y[t] >> 6) & 0x03030303u;
             }
             const int d0 = r >> 2, sh = r & 3;
-            for (int j = sid; j < r; j += NS) {
-                uint32_t cw[(B + 3) / 4 + 1];  // the dwords holding bytes r .. r+B-1 of row j
+            constexpr int NC = (B + 3) / 4 + 1;  // the dwords holding bytes r .. r+B-1 of a row
+            // software-pipelined over this stripe's rows: row j+NS's words are read while row j's products run
+            uint32_t cw[NC], xj = 0;
+            int j = sid;
 #pragma unroll
-                for (int u = 0; u < (B + 3) / 4 + 1; ++u) cw[u] = d0 + u < D ? M.w[j * D + d0 + u] : 0u;
-                uint32_t qw[(B + 3) / 4];  // bytes r.. aligned to dword boundaries
+            for (int u = 0; u < NC; ++u) cw[u] = (j < r && d0 + u < D) ? M.w[j * D + d0 + u] : 0u;
+            if (j < r) xj = M.w[j * D + w];
+            for (; j < r; j += NS) {
+                uint32_t qw[NC - 1];  // bytes r.. aligned to dword boundaries
 #pragma unroll
-                for (int u = 0; u < (B + 3) / 4; ++u) qw[u] = __builtin_amdgcn_alignbyte(cw[u + 1], cw[u], sh);
-                uint32_t xj = M.w[j * D + w];
+                for (int u = 0; u < NC - 1; ++u) qw[u] = __builtin_amdgcn_alignbyte(cw[u + 1], cw[u], sh);
+                uint4 t4[B];
+                uint32_t t2[B];
 #pragma unroll
                 for (int t = 0; t < B; ++t) {  // no branch: pieces past c multiply by 0
                     const uint32_t qq = t < c ? (qw[t >> 2] >> (8 * (t & 3))) & 0xFFu : 0u;
-                    const uint4 t4 = *reinterpret_cast<const uint4 *>(tab + qq * kTabDw);
-                    const uint32_t t2 = tab[qq * kTabDw + 4];
-                    xj = xor3(xj, __builtin_amdgcn_perm(t4.y, t4.x, ys[t].s0),
-                              xor3(__builtin_amdgcn_perm(t4.w, t4.z, ys[t].s1), __builtin_amdgcn_perm(t2, t2, ys[t].s2), 0u));
+                    t4[t] = *reinterpret_cast<const uint4 *>(tab + qq * kTabDw);
+                    t2[t] = tab[qq * kTabDw + 4];
                 }
+                const int jn = j + NS;
+                uint32_t cwn[NC], xjn = 0;
+#pragma unroll
+                for (int u = 0; u < NC; ++u) cwn[u] = (jn < r && d0 + u < D) ? M.w[jn * D + d0 + u] : 0u;
+                if (jn < r) xjn = M.w[jn * D + w];
+#pragma unroll
+                for (int t = 0; t < B; ++t)
+                    xj = xor3(xj, __builtin_amdgcn_perm(t4[t].y, t4[t].x, ys[t].s0),
+                              xor3(__builtin_amdgcn_perm(t4[t].w, t4[t].z, ys[t].s1), __builtin_amdgcn_perm(t2[t], t2[t], ys[t].s2), 0u));
                 M.w[j * D + w] = xj;
+#pragma unroll
+                for (int u = 0; u < NC; ++u) cw[u] = cwn[u];
+                xj = xjn;
             }
             if (wave == 0 && g == 0) {
 #pragma unroll
@@ -1309,7 +1342,7 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
     }
 }
 
-constexpr int kBlkNW = 4, kBlkB = 16;
+constexpr int kBlkNW = 4, kBlkB = 16, kBlkDefault = 8;
 
 size_t rref_block_lds_bytes(int k, int m) {
     const int D = rref_row_dwords(k, m);
@@ -1332,6 +1365,14 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     // the blocked clean run (4 waves per object, the default) when the row fits one wave (k + m <= 256)
     if ((p.lds_only == 0 || p.lds_only == 3) && rref_row_dwords(p.k, p.m) <= 64 &&
         rref_block_lds_bytes(p.k, p.m) <= kRrefMaxLds) {
+        // A/B knob (read once): RLNC_BLK = 8 or 16 pieces per block (NW = 4 waves)
+        // A/B knob (read once): RLNC_BLK = 8 or 16 pieces per block (profiles/r02_elim_ab.txt)
+        static const int blk = [] {
+            const char *e = getenv("RLNC_BLK");
+            const int v = e ? atoi(e) : kBlkDefault;
+            return v == 8 || v == 16 ? v : kBlkDefault;
+        }();
+        auto kern = blk == 16 ? &gf_rref_block_kernel<kBlkNW, 16> : &gf_rref_block_kernel<kBlkNW, 8>;
         static std::mutex mu;
         static bool attr_set[64] = {};
         int dev = 0;
@@ -1341,14 +1382,15 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
         {
             std::lock_guard<std::mutex> lock(mu);
             if (!attr_set[dev]) {
-                e = hipFuncSetAttribute(reinterpret_cast<const void *>(&gf_rref_block_kernel<kBlkNW, kBlkB>),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(kRrefMaxLds));
-                if (e != hipSuccess) return e;
+                for (auto f : {&gf_rref_block_kernel<kBlkNW, 8>, &gf_rref_block_kernel<kBlkNW, 16>}) {
+                    e = hipFuncSetAttribute(reinterpret_cast<const void *>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            int(kRrefMaxLds));
+                    if (e != hipSuccess) return e;
+                }
                 attr_set[dev] = true;
             }
         }
-        hipLaunchKernelGGL((gf_rref_block_kernel<kBlkNW, kBlkB>), dim3(p.n_obj), dim3(64 * kBlkNW),
-                           rref_block_lds_bytes(p.k, p.m), s, p);
+        hipLaunchKernelGGL(kern, dim3(p.n_obj), dim3(64 * kBlkNW), rref_block_lds_bytes(p.k, p.m), s, p);
         return hipGetLastError();
     }
     size_t lds = rref_lds_bytes(p.k, p.m);

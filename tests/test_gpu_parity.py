@@ -411,6 +411,27 @@ def test_decode_blocked_path_stress(ctx, k, m, sparsity, dep):
         assert not got[o, pay.shape[0]:].any()
 
 
+def test_decode_batch_many_objects(ctx):
+    """160 objects in one batch decode (one elimination launch of 160 workgroups, one product); every object's
+    statuses, payload rows and final status against the oracle."""
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(160)
+    nobj, k, m, L = 160, 16, 20, 64
+    seqs = _sequences(rng, nobj, k, m, L, 0.2, 0.1)
+    decoded = dev(np.zeros((nobj, k, L), np.uint8))
+    pst, ost, dl = batch.decode_batch(dev(seqs), k, decoded, ctx)
+    got = host(decoded)
+    for o in range(nobj):
+        od = OracleDecoder(L, k)
+        want = [S[od.decode(p)] for p in seqs[o]]
+        assert [S[x] for x in pst[o]] == want, o
+        pay = od.padded_payload()
+        assert np.array_equal(got[o, : pay.shape[0]], pay), o
+        st, data = od.get_decoded_data()
+        assert S[ost[o]] == S[st], o
+
+
 def test_decode_batch_device_async_outputs(ctx, orc):
     import torch
 
