@@ -133,21 +133,30 @@ struct rlnc_context {
     std::atomic<bool> graph_bound{false};
     std::mutex pool_mu;
     std::vector<std::unique_ptr<CallWs>> pool;
-    std::vector<rlnc_context *> subs;  // per-slot sub-contexts of the host-stream pipeline (host_stream.cpp)
-    DevBuf hs_din, hs_dcoef, hs_dout, hs_dst;  // as a host-stream slot: window buffers, kept between calls
-    PinBuf hs_hin, hs_hout, hs_hst;
+    // host-stream pipeline (host_stream.cpp): per-slot window buffers and the two copy streams, kept between calls.
+    // Few streams on purpose: HIP multiplexes streams over GPU_MAX_HW_QUEUES (4) hardware queues, and a copy
+    // stream sharing a queue with another stage serialises behind it.
+    struct HsSlot {
+        DevBuf din, dcoef, dout, dst;
+        PinBuf hin, hout, hst;
+    };
+    std::vector<std::unique_ptr<HsSlot>> hs_slots;
+    hipStream_t hs_h2d = nullptr, hs_d2h = nullptr;
     DevBuf ws_tab;  // descriptor tables of the wire-format calls (wire.hip), uploaded from pin_tab
     PinBuf pin_tab;
     hipEvent_t tab_ev = nullptr;  // the last descriptor upload (pin_tab may be rewritten once it has run)
 
-    int sub_context(size_t i, rlnc_context **out);
     void retain() { refs.fetch_add(1, std::memory_order_relaxed); }
     void release() {
         if (refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
-        for (rlnc_context *c : subs)
-            if (c) c->release();
         (void)hipSetDevice(device);
         (void)hipStreamSynchronize(stream);
+        for (hipStream_t x : {hs_h2d, hs_d2h})
+            if (x) {
+                (void)hipStreamSynchronize(x);
+                (void)hipStreamDestroy(x);
+            }
+        hs_slots.clear();
         if (tab_ev) (void)hipEventDestroy(tab_ev);
         if (own) (void)hipStreamDestroy(own);
         delete this;  // the buffers' destructors free on this device

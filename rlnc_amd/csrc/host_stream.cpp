@@ -1,13 +1,20 @@
 // host_stream.cpp — pieces that start and end in host memory (a socket or a file), SURVEY.md §8(f1).
 //
 // rlnc_encode_host_stream / rlnc_decode_host_stream stream a batch of objects through the device in windows of
-// objects.  Three pipeline slots, each with its own stream, device buffers and (for pageable host memory) pinned
-// staging: window w's host→device copy, its encode/decode and its device→host copy run on slot w % 3's stream,
-// so the copy engines (both PCIe directions) and the compute of consecutive windows overlap.  Host buffers that
-// are already pinned (hipHostMalloc / hipHostRegister) are copied by DMA directly; pageable ones are staged
-// through the slot's pinned buffers by host threads (a multi-threaded memcpy runs while the device works on the
-// other two slots).  The device work is the batch API itself (rlnc_encode_batch, rlnc_decode_batch_device) on
-// one sub-context per slot, so results are bit-identical to the device-resident path.
+// objects, as a three-stage pipeline on three streams: every host→device copy on one stream, every encode/decode
+// on a compute stream, every device→host copy on a third, ordered per window by events.  Each direction's DMA
+// engine is fed back to back (copies of consecutive windows are adjacent on their stream), and the compute of
+// window w overlaps the copies of its neighbours.  Windows rotate over `n` slots of device buffers (and, for
+// pageable host memory, pinned staging); a slot is refilled only after the kernel that read its input and the copy
+// that read its output have run (event waits on the device, no host round trip).  Three streams in all (the
+// context's own for the compute, one per copy direction): HIP multiplexes streams over GPU_MAX_HW_QUEUES (4)
+// hardware queues, and a copy stream sharing a queue with another stage serialises behind it (measured: a
+// sub-context and stream per slot made the decode call's copies erratic, 44-89 GB/s).  Host buffers that are already
+// pinned (hipHostMalloc / hipHostRegister) are copied by DMA directly and the host thread never blocks until the
+// end; pageable ones are staged through the slot's pinned buffers by host threads (a multi-threaded memcpy runs
+// while the device works on the other slots).  The device work is the batch API itself (rlnc_encode_batch,
+// rlnc_decode_batch_device) on the context, so results are bit-identical to the device-resident path.
+#include <cstdlib>
 #include <thread>
 
 #include "context.hpp"
@@ -16,7 +23,17 @@ using namespace rlnc::eng;
 
 namespace {
 
-constexpr int kSlots = 3;
+constexpr int kDefaultSlots = 3;  // profiles/r02_host_stream_ab.txt
+constexpr int kMaxSlots = 8;
+// pipeline slots (windows in flight); RLNC_HS_SLOTS (A/B knob, read once) overrides the default
+int num_slots() {
+    static const int n = [] {
+        const char *e = getenv("RLNC_HS_SLOTS");
+        const int v = e ? atoi(e) : kDefaultSlots;
+        return v >= 2 && v <= kMaxSlots ? v : kDefaultSlots;
+    }();
+    return n;
+}
 
 bool is_pinned(const void *p) {
     hipPointerAttribute_t a;
@@ -61,59 +78,80 @@ void copy_rows(uint8_t *dst, size_t dst_stride, const uint8_t *src, size_t src_s
     for (auto &t : th) t.join();
 }
 
+using HsSlot = rlnc_context::HsSlot;
+
 struct Slot {
-    rlnc_context *ctx = nullptr;  // sub-context: own stream and workspaces; its hs_* buffers are this slot's
-    hipEvent_t done = nullptr;
-    size_t w0 = 0, w1 = 0;  // objects of the window in flight
+    HsSlot *buf = nullptr;                                          // the context's window buffers of this slot
+    hipEvent_t hdone = nullptr, kdone = nullptr, ddone = nullptr;  // its last H2D / kernel / D2H
+    size_t w0 = 0, w1 = 0;                                          // objects of the window it holds
     bool busy = false;
 };
 
 struct Pipeline {
-    rlnc_context *parent;
-    Slot slot[kSlots];
-    explicit Pipeline(rlnc_context *p) : parent(p) {}
+    rlnc_context *comp;  // compute stage: the context itself (its stream, its batch workspaces)
+    hipStream_t h2d = nullptr, d2h = nullptr;
+    Slot slot[kMaxSlots];
+    const int n = num_slots();
+    explicit Pipeline(rlnc_context *c) : comp(c) {}
     int init() {
-        for (auto &s : slot) {
-            int st = parent->sub_context(&s - slot, &s.ctx);
-            if (st) return st;
-            HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        {
+            std::lock_guard<std::mutex> lock(comp->pool_mu);
+            if (!comp->hs_h2d) HIP_TRY(hipStreamCreateWithFlags(&comp->hs_h2d, hipStreamNonBlocking));
+            if (!comp->hs_d2h) HIP_TRY(hipStreamCreateWithFlags(&comp->hs_d2h, hipStreamNonBlocking));
+            while (comp->hs_slots.size() < size_t(n)) comp->hs_slots.emplace_back(new HsSlot);
+        }
+        h2d = comp->hs_h2d;
+        d2h = comp->hs_d2h;
+        // the copy stages start after the work already enqueued on the context stream
+        hipEvent_t start;
+        HIP_TRY(hipEventCreateWithFlags(&start, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(start, comp->stream));
+        HIP_TRY(hipStreamWaitEvent(h2d, start, 0));
+        HIP_TRY(hipStreamWaitEvent(d2h, start, 0));
+        (void)hipEventDestroy(start);
+        for (int i = 0; i < n; ++i) {
+            Slot &s = slot[i];
+            s.buf = comp->hs_slots[size_t(i)].get();
+            HIP_TRY(hipEventCreateWithFlags(&s.hdone, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s.kdone, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s.ddone, hipEventDisableTiming));
         }
         return RLNC_OK;
     }
+    // slot s may take window w: its previous window's kernel has read the input buffers (H2D waits on kdone) and
+    // its D2H has read the output buffers (the kernel waits on ddone)
+    int before_h2d(Slot &s) {
+        if (s.busy) HIP_TRY(hipStreamWaitEvent(h2d, s.kdone, 0));
+        return RLNC_OK;
+    }
+    int before_kernel(Slot &s) {
+        HIP_TRY(hipStreamWaitEvent(comp->stream, s.hdone, 0));
+        if (s.busy) HIP_TRY(hipStreamWaitEvent(comp->stream, s.ddone, 0));
+        return RLNC_OK;
+    }
+    int before_d2h(Slot &s) {
+        HIP_TRY(hipStreamWaitEvent(d2h, s.kdone, 0));
+        return RLNC_OK;
+    }
     ~Pipeline() {
-        for (auto &s : slot) {
-            if (s.done) {
-                (void)hipEventSynchronize(s.done);
-                (void)hipEventDestroy(s.done);
-            }
-        }
+        if (d2h) (void)hipStreamSynchronize(d2h);
+        (void)hipStreamSynchronize(comp->stream);
+        if (h2d) (void)hipStreamSynchronize(h2d);
+        for (auto &s : slot)
+            for (hipEvent_t e : {s.hdone, s.kdone, s.ddone})
+                if (e) (void)hipEventDestroy(e);
     }
 };
 
-size_t auto_window(size_t bytes_per_object, size_t nobj) {
-    // >= 64 MiB of input per window (PCIe copies of that size run at full rate), at most a third of the batch
-    // so that the three slots overlap
-    size_t w = std::max<size_t>(1, (size_t(64) << 20) / std::max<size_t>(1, bytes_per_object));
-    w = std::min(w, std::max<size_t>(1, (nobj + 2) / 3));
+size_t auto_window(size_t bytes_per_object, size_t nobj, int slots) {
+    // >= 32 MiB of input per window (PCIe copies of that size run at full rate), at most 1/slots of the batch
+    // so that the slots overlap (profiles/r02_host_stream_ab.txt)
+    size_t w = std::max<size_t>(1, (size_t(32) << 20) / std::max<size_t>(1, bytes_per_object));
+    w = std::min(w, std::max<size_t>(1, (nobj + slots - 1) / slots));
     return std::min(w, nobj);
 }
 
 }  // namespace
-
-// sub-context `i` of a context (created on first use, owned by the parent, same device and kernel settings)
-int rlnc_context::sub_context(size_t i, rlnc_context **out) {
-    std::lock_guard<std::mutex> lock(pool_mu);
-    if (subs.size() <= i) subs.resize(i + 1, nullptr);
-    if (!subs[i]) {
-        int st = rlnc_context_create(device, &subs[i]);
-        if (st) return st;
-    }
-    subs[i]->variant = variant;
-    subs[i]->max_tile_rows = max_tile_rows;
-    subs[i]->decode_path = decode_path;
-    *out = subs[i];
-    return RLNC_OK;
-}
 
 extern "C" {
 
@@ -126,53 +164,59 @@ int rlnc_encode_host_stream(rlnc_context *ctx, const uint8_t *src, size_t k, siz
     CHECK_ARG(src && coeffs && pieces);
     int st = ctx->activate();
     if (st) return st;
-    HIP_TRY(hipStreamSynchronize(ctx->stream));  // earlier work on the context is done (synchronous call)
     const size_t full = k + L, in_b = k * L, co_b = n * k, out_b = n * full;
-    const size_t W = window ? std::min(window, nobj) : auto_window(in_b, nobj);
     const bool pin_in = is_pinned(src) && is_pinned(coeffs), pin_out = is_pinned(pieces);
     Pipeline pl(ctx);
     if ((st = pl.init())) return st;
-    for (auto &s : pl.slot) {
-        if ((st = s.ctx->hs_din.ensure(W * in_b)) || (st = s.ctx->hs_dcoef.ensure(W * co_b)) || (st = s.ctx->hs_dout.ensure(W * out_b)))
+    const size_t W = window ? std::min(window, nobj) : auto_window(in_b, nobj, pl.n);
+    for (int i = 0; i < pl.n; ++i) {
+        HsSlot *b = pl.slot[i].buf;
+        if ((st = b->din.ensure(W * in_b)) || (st = b->dcoef.ensure(W * co_b)) || (st = b->dout.ensure(W * out_b)))
             return st;
-        if (!pin_in && ((st = s.ctx->hs_hin.ensure(W * (in_b + co_b))))) return st;
-        if (!pin_out && (st = s.ctx->hs_hout.ensure(W * out_b))) return st;
+        if (!pin_in && ((st = b->hin.ensure(W * (in_b + co_b))))) return st;
+        if (!pin_out && (st = b->hout.ensure(W * out_b))) return st;
     }
-    auto retire = [&](Slot &s) -> int {  // the slot's window is done; pageable output copied out
-        if (!s.busy) return RLNC_OK;
-        HIP_TRY(hipEventSynchronize(s.done));
-        if (!pin_out) copy_rows(pieces + s.w0 * out_b, 0, s.ctx->hs_hout.as<uint8_t>(), 0, (s.w1 - s.w0) * out_b, 1);
-        s.busy = false;
+    auto retire = [&](Slot &s) -> int {  // pageable output: the slot's coded pieces copied out of its staging
+        if (!s.busy || pin_out) return RLNC_OK;
+        HIP_TRY(hipEventSynchronize(s.ddone));
+        copy_rows(pieces + s.w0 * out_b, 0, s.buf->hout.as<uint8_t>(), 0, (s.w1 - s.w0) * out_b, 1);
         return RLNC_OK;
     };
     size_t w = 0;
     for (size_t o0 = 0; o0 < nobj; o0 += W, ++w) {
-        Slot &s = pl.slot[w % kSlots];
+        Slot &s = pl.slot[w % pl.n];
+        HsSlot *b = s.buf;
         if ((st = retire(s))) return st;
-        const size_t o1 = std::min(nobj, o0 + W), b = o1 - o0;
-        hipStream_t hs = s.ctx->stream;
+        const size_t o1 = std::min(nobj, o0 + W), cnt = o1 - o0;
         const uint8_t *hin = src + o0 * in_b, *hco = coeffs + o0 * co_b;
-        if (!pin_in) {  // stage through the slot's pinned buffer (host threads), then DMA
-            uint8_t *h = s.ctx->hs_hin.as<uint8_t>();
-            copy_rows(h, 0, hin, 0, b * in_b, 1);
-            std::memcpy(h + b * in_b, hco, b * co_b);
+        if (!pin_in) {  // stage through the slot's pinned buffer once its previous H2D has read it
+            if (s.busy) HIP_TRY(hipEventSynchronize(s.hdone));
+            uint8_t *h = b->hin.as<uint8_t>();
+            copy_rows(h, 0, hin, 0, cnt * in_b, 1);
+            std::memcpy(h + cnt * in_b, hco, cnt * co_b);
             hin = h;
-            hco = h + b * in_b;
+            hco = h + cnt * in_b;
         }
-        HIP_TRY(hipMemcpyAsync(s.ctx->hs_din.p, hin, b * in_b, hipMemcpyHostToDevice, hs));
-        HIP_TRY(hipMemcpyAsync(s.ctx->hs_dcoef.p, hco, b * co_b, hipMemcpyHostToDevice, hs));
-        if ((st = rlnc_encode_batch(s.ctx, s.ctx->hs_din.as<uint8_t>(), k, L, b, s.ctx->hs_dcoef.as<uint8_t>(), n,
-                                    s.ctx->hs_dout.as<uint8_t>())))
+        if ((st = pl.before_h2d(s))) return st;
+        HIP_TRY(hipMemcpyAsync(b->din.p, hin, cnt * in_b, hipMemcpyHostToDevice, pl.h2d));
+        HIP_TRY(hipMemcpyAsync(b->dcoef.p, hco, cnt * co_b, hipMemcpyHostToDevice, pl.h2d));
+        HIP_TRY(hipEventRecord(s.hdone, pl.h2d));
+        if ((st = pl.before_kernel(s))) return st;
+        if ((st = rlnc_encode_batch(pl.comp, b->din.as<uint8_t>(), k, L, cnt, b->dcoef.as<uint8_t>(), n,
+                                    b->dout.as<uint8_t>())))
             return st;
-        HIP_TRY(hipMemcpyAsync(pin_out ? pieces + o0 * out_b : s.ctx->hs_hout.as<uint8_t>(), s.ctx->hs_dout.p, b * out_b,
-                               hipMemcpyDeviceToHost, hs));
-        HIP_TRY(hipEventRecord(s.done, hs));
+        HIP_TRY(hipEventRecord(s.kdone, pl.comp->stream));
+        if ((st = pl.before_d2h(s))) return st;
+        HIP_TRY(hipMemcpyAsync(pin_out ? pieces + o0 * out_b : b->hout.as<uint8_t>(), b->dout.p, cnt * out_b,
+                               hipMemcpyDeviceToHost, pl.d2h));
+        HIP_TRY(hipEventRecord(s.ddone, pl.d2h));
         s.w0 = o0;
         s.w1 = o1;
         s.busy = true;
     }
-    for (size_t i = 0; i < kSlots; ++i)  // drain in window order
-        if ((st = retire(pl.slot[(w + i) % kSlots]))) return st;
+    for (size_t i = 0; i < size_t(pl.n); ++i)  // drain in window order
+        if ((st = retire(pl.slot[(w + i) % pl.n]))) return st;
+    HIP_TRY(hipStreamSynchronize(pl.d2h));
     return RLNC_OK;
 }
 
@@ -190,76 +234,86 @@ int rlnc_decode_host_stream(rlnc_context *ctx, const uint8_t *pieces, size_t obj
     const bool dev_elim = rlnc::rref_lds_bytes(int(k), int(m)) <= rlnc::kRrefMaxLds && ctx->decode_path != 1;
     int st = ctx->activate();
     if (st) return st;
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    const size_t W = window ? std::min(window, nobj) : auto_window(in_b, nobj);
     const bool pin_in = is_pinned(pieces), pin_out = is_pinned(decoded);
     const size_t st_b = 8 + m * 4 + 4;  // per object: length (int64, first: aligned), piece statuses, object status
     Pipeline pl(ctx);
     if ((st = pl.init())) return st;
-    for (auto &s : pl.slot) {
-        if ((st = s.ctx->hs_din.ensure(W * in_b)) || (st = s.ctx->hs_dout.ensure(W * out_b)) || (st = s.ctx->hs_dst.ensure(W * st_b)) ||
-            (st = s.ctx->hs_hst.ensure(W * st_b)))
+    const size_t W = window ? std::min(window, nobj) : auto_window(in_b, nobj, pl.n);
+    for (int i = 0; i < pl.n; ++i) {
+        HsSlot *b = pl.slot[i].buf;
+        if ((st = b->din.ensure(W * in_b)) || (st = b->dout.ensure(W * out_b)) || (st = b->dst.ensure(W * st_b)) ||
+            (st = b->hst.ensure(W * st_b)))
             return st;
-        if (!pin_in && (st = s.ctx->hs_hin.ensure(W * in_b))) return st;
-        if (!pin_out && (st = s.ctx->hs_hout.ensure(W * out_b))) return st;
+        if (!pin_in && (st = b->hin.ensure(W * in_b))) return st;
+        if (!pin_out && (st = b->hout.ensure(W * out_b))) return st;
     }
-    auto retire = [&](Slot &s) -> int {
+    auto retire = [&](Slot &s) -> int {  // the slot's window is out: statuses (and pageable payload) copied out
         if (!s.busy) return RLNC_OK;
-        HIP_TRY(hipEventSynchronize(s.done));
-        const size_t b = s.w1 - s.w0;
-        if (!pin_out) copy_rows(decoded + s.w0 * out_b, 0, s.ctx->hs_hout.as<uint8_t>(), 0, b * out_b, 1);
+        HIP_TRY(hipEventSynchronize(s.ddone));
+        const size_t cnt = s.w1 - s.w0;
+        if (!pin_out) copy_rows(decoded + s.w0 * out_b, 0, s.buf->hout.as<uint8_t>(), 0, cnt * out_b, 1);
         if (dev_elim) {
-            const uint8_t *h = s.ctx->hs_hst.as<uint8_t>();
+            const uint8_t *h = s.buf->hst.as<uint8_t>();
             const int64_t *dl = reinterpret_cast<const int64_t *>(h);
-            const int32_t *ps = reinterpret_cast<const int32_t *>(h + b * 8);
-            const int32_t *os = reinterpret_cast<const int32_t *>(h + b * 8 + b * m * 4);
-            for (size_t o = 0; o < b; ++o) {
+            const int32_t *ps = reinterpret_cast<const int32_t *>(h + cnt * 8);
+            const int32_t *os = reinterpret_cast<const int32_t *>(h + cnt * 8 + cnt * m * 4);
+            for (size_t o = 0; o < cnt; ++o) {
                 if (object_status) object_status[s.w0 + o] = os[o];
                 if (data_len) data_len[s.w0 + o] = uint64_t(os[o] == 0 ? dl[o] : 0);
             }
-            if (piece_status) std::memcpy(piece_status + s.w0 * m, ps, b * m * 4);
+            if (piece_status) std::memcpy(piece_status + s.w0 * m, ps, cnt * m * 4);
         }
-        s.busy = false;
         return RLNC_OK;
     };
     size_t w = 0;
     for (size_t o0 = 0; o0 < nobj; o0 += W, ++w) {
-        Slot &s = pl.slot[w % kSlots];
+        Slot &s = pl.slot[w % pl.n];
+        HsSlot *b = s.buf;
         if ((st = retire(s))) return st;
-        const size_t o1 = std::min(nobj, o0 + W), b = o1 - o0;
-        hipStream_t hs = s.ctx->stream;
-        uint8_t *dout = s.ctx->hs_dout.as<uint8_t>();
-        if (pin_in) {  // the first m pieces of each object, strided by obj_stride, straight from pinned memory
-            HIP_TRY(hipMemcpy2DAsync(s.ctx->hs_din.p, in_b, pieces + o0 * obj_stride, obj_stride, in_b, b,
-                                     hipMemcpyHostToDevice, hs));
-        } else {
-            copy_rows(s.ctx->hs_hin.as<uint8_t>(), in_b, pieces + o0 * obj_stride, obj_stride, in_b, b);
-            HIP_TRY(hipMemcpyAsync(s.ctx->hs_din.p, s.ctx->hs_hin.p, b * in_b, hipMemcpyHostToDevice, hs));
+        const size_t o1 = std::min(nobj, o0 + W), cnt = o1 - o0;
+        uint8_t *dout = b->dout.as<uint8_t>();
+        if (!pin_in) {  // the first m pieces of each object into the slot's staging (its previous H2D is done)
+            if (s.busy) HIP_TRY(hipEventSynchronize(s.hdone));
+            copy_rows(b->hin.as<uint8_t>(), in_b, pieces + o0 * obj_stride, obj_stride, in_b, cnt);
         }
+        if ((st = pl.before_h2d(s))) return st;
+        if (pin_in) {  // strided by obj_stride, straight from pinned memory: one linear copy per object (the 2D
+                       // copy measured erratic, 44-89 GB/s)
+            for (size_t o = 0; o < cnt; ++o)
+                HIP_TRY(hipMemcpyAsync(b->din.as<uint8_t>() + o * in_b, pieces + (o0 + o) * obj_stride, in_b,
+                                       hipMemcpyHostToDevice, pl.h2d));
+        } else {
+            HIP_TRY(hipMemcpyAsync(b->din.p, b->hin.p, cnt * in_b, hipMemcpyHostToDevice, pl.h2d));
+        }
+        HIP_TRY(hipEventRecord(s.hdone, pl.h2d));
+        if ((st = pl.before_kernel(s))) return st;
         if (dev_elim) {
-            uint8_t *dst = s.ctx->hs_dst.as<uint8_t>();
+            uint8_t *dst = b->dst.as<uint8_t>();
             int64_t *dl = reinterpret_cast<int64_t *>(dst);
-            int32_t *ps = reinterpret_cast<int32_t *>(dst + b * 8);
-            int32_t *os = reinterpret_cast<int32_t *>(dst + b * 8 + b * m * 4);
-            if ((st = rlnc_decode_batch_device(s.ctx, s.ctx->hs_din.as<uint8_t>(), in_b, k, L, m, b, dout, ps, os, dl)))
+            int32_t *ps = reinterpret_cast<int32_t *>(dst + cnt * 8);
+            int32_t *os = reinterpret_cast<int32_t *>(dst + cnt * 8 + cnt * m * 4);
+            if ((st = rlnc_decode_batch_device(pl.comp, b->din.as<uint8_t>(), in_b, k, L, m, cnt, dout, ps, os, dl)))
                 return st;
-            HIP_TRY(hipMemcpyAsync(s.ctx->hs_hst.p, dst, b * st_b, hipMemcpyDeviceToHost, hs));
         } else {  // elimination too large for LDS: the host-elimination batch path (synchronous per window)
-            if ((st = rlnc_decode_batch(s.ctx, s.ctx->hs_din.as<uint8_t>(), in_b, k, L, m, b, dout,
+            if ((st = rlnc_decode_batch(pl.comp, b->din.as<uint8_t>(), in_b, k, L, m, cnt, dout,
                                         piece_status ? piece_status + o0 * m : nullptr,
                                         object_status ? object_status + o0 : nullptr,
                                         data_len ? data_len + o0 : nullptr)))
                 return st;
         }
-        HIP_TRY(hipMemcpyAsync(pin_out ? decoded + o0 * out_b : s.ctx->hs_hout.as<uint8_t>(), dout, b * out_b,
-                               hipMemcpyDeviceToHost, hs));
-        HIP_TRY(hipEventRecord(s.done, hs));
+        HIP_TRY(hipEventRecord(s.kdone, pl.comp->stream));
+        if ((st = pl.before_d2h(s))) return st;
+        if (dev_elim) HIP_TRY(hipMemcpyAsync(b->hst.p, b->dst.p, cnt * st_b, hipMemcpyDeviceToHost, pl.d2h));
+        HIP_TRY(hipMemcpyAsync(pin_out ? decoded + o0 * out_b : b->hout.as<uint8_t>(), dout, cnt * out_b,
+                               hipMemcpyDeviceToHost, pl.d2h));
+        HIP_TRY(hipEventRecord(s.ddone, pl.d2h));
         s.w0 = o0;
         s.w1 = o1;
         s.busy = true;
     }
-    for (size_t i = 0; i < kSlots; ++i)
-        if ((st = retire(pl.slot[(w + i) % kSlots]))) return st;
+    for (size_t i = 0; i < size_t(pl.n); ++i)
+        if ((st = retire(pl.slot[(w + i) % pl.n]))) return st;
+    HIP_TRY(hipStreamSynchronize(pl.d2h));
     return RLNC_OK;
 }
 

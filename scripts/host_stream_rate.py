@@ -11,6 +11,10 @@ and receives does it, the encode of step i and the decode of step i-1 as two con
 on two contexts (pinned, "concurrent": two buffer sets, so both PCIe directions carry traffic at once).  Reports GiB/s in bench.py's counters, the PCIe bytes moved, the raw
 pinned copy rates of the box, and checks decoded == source for every object.
 """
+# HIP multiplexes streams over GPU_MAX_HW_QUEUES hardware queues (4 by default); the library's pipeline keeps three
+# streams busy (compute, host->device, device->host), and with 4 queues a copy stream can share a queue with another
+# stage of this process.  Run it as `GPU_MAX_HW_QUEUES=16 python scripts/host_stream_rate.py` to give every stream
+# its own queue (profiles/r02_host_stream_ab.txt has both); the value in use is reported.
 import argparse
 import ctypes as C
 import json
@@ -39,7 +43,8 @@ def main():
     lib = ctx.lib
     rng = np.random.default_rng(1)
     out = {"metric": "host-resident RLNC encode+decode GiB/s (library pipeline, host buffers in and out), "
-                     "k=32 x 1 MiB", "unit": "GiB/s", "objects": B}
+                     "k=32 x 1 MiB", "unit": "GiB/s", "objects": B,
+           "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)")}
     for mode in ("pinned", "pageable"):
         pin = mode == "pinned"
 
@@ -54,14 +59,21 @@ def main():
         dl = np.zeros(B, np.uint64)
         p = lambda t: C.c_void_p(t.data_ptr())
 
+        part = {"encode": 0.0, "decode": 0.0}
+
         def step():
+            t = time.perf_counter()
             assert lib.rlnc_encode_host_stream(ctx.h, p(src), k, L, B, p(co), n, p(pieces), args.window) == 0
+            t2 = time.perf_counter()
             assert lib.rlnc_decode_host_stream(ctx.h, p(pieces), n * (k + L), k, L, m, B, p(dec),
                                                ps.ctypes.data_as(C.POINTER(C.c_int32)),
                                                os_.ctypes.data_as(C.POINTER(C.c_int32)),
                                                dl.ctypes.data_as(C.POINTER(C.c_uint64)), args.window) == 0
+            part["encode"] += t2 - t
+            part["decode"] += time.perf_counter() - t2
 
         step()  # warm-up: the library's pipeline buffers are allocated once and kept
+        part["encode"] = part["decode"] = 0.0
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
@@ -70,7 +82,11 @@ def main():
         moved = B * (k * L + n * k + n * (k + L) + m * (k + L) + k * L)
         out[mode] = {"value": round(bench.step_bytes(B, k, L, n) / el / 2**30, 2), "ms_per_step": round(el * 1e3, 2),
                      "pcie_bytes_per_step": moved, "pcie_GBps_effective": round(moved / el / 1e9, 2),
-                     "roundtrip_goodput_GiBps": round(B * k * L / el / 2**30, 3), "verified": bool(ok)}
+                     "roundtrip_goodput_GiBps": round(B * k * L / el / 2**30, 3), "verified": bool(ok),
+                     "encode_call_ms": round(part["encode"] / args.steps * 1e3, 2),
+                     "encode_call_GBps": round(B * (k * L + n * k + n * (k + L)) / (part["encode"] / args.steps) / 1e9, 2),
+                     "decode_call_ms": round(part["decode"] / args.steps * 1e3, 2),
+                     "decode_call_GBps": round(B * (m * (k + L) + k * L) / (part["decode"] / args.steps) / 1e9, 2)}
         del src, co, pieces, dec
     # concurrent: step i's encode (thread A, context A) beside step i-1's decode (thread B, context B); ctypes releases
     # the GIL inside the library, so the two calls overlap on the device and on PCIe
@@ -119,6 +135,26 @@ def main():
                          "roundtrip_goodput_GiBps": round(B * k * L / el / 2**30, 3), "verified": bool(ok),
                          "how": "encode of step i and decode of step i-1 from two host threads on two contexts"}
     del src, co, pieces, dec
+    # the bidirectional ceiling: 1 GiB host->device and 1 GiB device->host at once on two streams
+    h_a = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+    h_b = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+    d_a = torch.empty(1 << 30, dtype=torch.uint8, device="cuda:0")
+    d_b = torch.empty(1 << 30, dtype=torch.uint8, device="cuda:0")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for it in range(2):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        with torch.cuda.stream(s1):
+            d_a.copy_(h_a, non_blocking=True)
+        with torch.cuda.stream(s2):
+            h_b.copy_(d_b, non_blocking=True)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t
+    out["pinned_bidirectional_GBps"] = round(2 * (1 << 30) / el / 1e9, 2)
+    for mode in ("pinned", "pageable", "concurrent"):
+        if mode in out:
+            out[mode]["frac_of_bidirectional"] = round(out[mode]["pcie_GBps_effective"] / out["pinned_bidirectional_GBps"], 4)
+    del h_a, h_b, d_a, d_b
     # raw pinned copy rates of this box
     big_h = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
     big_d = torch.empty(1 << 30, dtype=torch.uint8, device="cuda:0")
