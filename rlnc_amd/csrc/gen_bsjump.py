@@ -49,6 +49,12 @@ WAVES = 4  # waves per workgroup (all on the same 4 KiB column chunk)
 WG_ROWS = NT * WAVES
 SLOTS = 3  # LDS ring slots of 4 KiB (rows j, j+1, j+2)
 BLOCK_BYTES = 16 * 8 + 4  # 16 VOP3 (8 bytes) + s_setpc_b64 (4 bytes); --stride pads with s_nop (never run)
+# Default layout: blocks on an 8-byte grid (stride 136, table 8-byte aligned) so that no 8-byte VOP3 straddles an
+# 8-byte boundary: encode launch -1.6 %, bench +0.9 % against stride 132; 256-byte-aligned blocks (a 64 KB table)
+# made the encode launch 12 % slower and 64-byte-aligned ones (stride 192) 5 %: instruction-cache capacity, not alignment, dominates in the
+# product kernel (profiles/r02_bsj_layout_ab.txt; the isolated call microbenchmark, scripts/ubench_tables.py, gains
+# 10 % from 256-byte alignment).
+DEFAULT_STRIDE, DEFAULT_ALIGN = 136, 3
 STREAM_J_BYTES = WG_ROWS * 4  # one dword (block offset) per row of the workgroup tile
 
 
@@ -475,6 +481,8 @@ def program_shared_body(cons=False):
     L += ["3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
     epilogue(L)
     L.append("s_branch 8f")
+    if ALIGN:
+        L.append(f".p2align {ALIGN}")
     L.append("9:")
     blocks(L)
     L.append("8:")
@@ -667,8 +675,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "bitslice_jump.inc"))
     ap.add_argument("--diag", default="", help="comma list: novm, inline, absinline (timing diagnostics, wrong results)")
-    ap.add_argument("--stride", type=int, default=BLOCK_BYTES, help="bytes per code block (>= 132, multiple of 4)")
-    ap.add_argument("--align", type=int, default=0, help="log2 alignment of the block table")
+    ap.add_argument("--stride", type=int, default=DEFAULT_STRIDE, help="bytes per code block (>= 132, multiple of 4)")
+    ap.add_argument("--align", type=int, default=DEFAULT_ALIGN, help="log2 alignment of the block table")
     ap.add_argument("--bar8", type=int, default=3, choices=(2, 3), help="8-wave program: a barrier every N rows")
     ap.add_argument("--prio8", default="off", help="K,L: 8-wave program's calls K.. of each row at s_setprio L")
     ap.add_argument("--prio", default="", help="K,L: shared program's calls K.. of each row at s_setprio L")

@@ -903,7 +903,11 @@ hipError_t launch_bs(const MatmulParams &p, hipStream_t s, void *scratch, size_t
 #ifdef RLNC_BSJ_ASM_FILE  // diagnostic builds substitute a generated variant
 #include RLNC_BSJ_ASM_FILE
 #else
+#ifdef RLNC_BSJ_INC  // A/B builds of the generated program (scripts/bsj_layout_ab.sh)
+#include RLNC_BSJ_INC
+#else
 #include "bitslice_jump.inc"
+#endif
 #endif
 
 constexpr int kBsjWaveRows = RLNC_BSJ_NT;  // output rows per wave; a workgroup of W waves = 8 W rows

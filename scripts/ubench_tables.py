@@ -40,55 +40,82 @@ def G(g, h, v):
     return 128 + g * 32 + h * 16 + v
 
 
-def blocks(slot, relative):
+def block_body(c, slot, relative, reps=1):
+    lo, hi = block_indices(c)
     L = []
-    for c in range(256):
-        lo, hi = block_indices(c)
-        n = 0
+    for _ in range(reps):
         for g in range(2):
             for o in range(8):
                 a = (0 if relative else slot * 16) + g * 8 + o
                 x = f"v{G(g, 0, lo[o])}" if lo[o] else "0"
                 y = f"v{G(g, 1, hi[o])}" if hi[o] else "0"
                 L.append(f"v_bitop3_b32 v{a}, {x}, {y}, v{a} bitop3:0x96")
-                n += 1
-        L.append("s_setpc_b64 s[40:41]")
     return L
 
 
+def blocks(slot, relative, reps=1, stride=None, empty=False):
+    """256 blocks; each 16 * reps XOR3s (none if empty) + s_setpc, padded with s_nop to `stride` bytes."""
+    L = []
+    size = (0 if empty else 16 * reps * 8) + 4
+    stride = stride or size
+    for c in range(256):
+        if not empty:
+            L += block_body(c, slot, relative, reps)
+        L.append("s_setpc_b64 s[40:41]")
+        L += ["s_nop 0"] * ((stride - size) // 4)
+    return L
+
+
+MODES = {  # name: (tables, relative, xor3 reps per block, stride, empty, inline)
+    "rel1": (1, True, 1, None, False, False),
+    "abs1": (1, False, 1, None, False, False),
+    "rel1_a256": (1, True, 1, 256, False, False),
+    "empty": (1, False, 1, None, True, False),
+    "rel1_x2": (1, True, 2, None, False, False),
+    "inline_rel": (0, True, 1, None, False, True),
+    "inline_abs": (0, False, 1, None, False, True),
+}
+
+
+def block_stride(mode):
+    tables, rel, reps, stride, empty, inl = MODES[mode]
+    size = (0 if empty else 16 * reps * 8) + 4
+    return stride or size
+
+
 def program(mode):
-    tables = 8 if mode == "abs8" else 1
-    # the tables sit first and the entry jumps over them with s_setpc (a 270 KB table is beyond s_branch's range)
+    tables, rel, reps, stride, empty, inl = MODES[mode]
+    bs = block_stride(mode)
+    # the tables sit first and the entry jumps over them with s_setpc (big tables are beyond s_branch's range)
     L = ["s_getpc_b64 s[36:37]", "2:", "s_add_u32 s36, s36, (9f - 2b)", "s_addc_u32 s37, s37, 0",
          "s_mov_b64 s[52:53], %[offs]", "s_mov_b32 s43, %[reps]",
          "s_getpc_b64 s[54:55]", "3:", "s_add_u32 s54, s54, (7f - 3b)", "s_addc_u32 s55, s55, 0",
-         "s_setpc_b64 s[54:55]", "9:"]
+         "s_setpc_b64 s[54:55]", ".p2align 8", "9:"]
     for t in range(tables):
-        L += blocks(t, mode == "rel1")
+        L += blocks(t, rel, reps, stride, empty)
     L.append("7:")
-    if mode == "rel1":
+    if rel:
         L.append("s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)")
     L.append("1:")
     L += ["s_load_dwordx8 s[44:51], s[52:53], 0", "s_add_u32 s52, s52, 32", "s_addc_u32 s53, s53, 0",
           "s_waitcnt lgkmcnt(0)"]
     for i in range(8):
-        if mode == "rel1":
+        if rel:
             L.append(f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}")
-        # table t's block c at base + t * 256 * BLOCK + c * BLOCK (the offsets hold c * BLOCK)
-        t = i if mode == "abs8" else 0
-        L += [f"s_add_u32 s38, s36, s{44 + i}", "s_addc_u32 s39, s37, 0"]
-        if t:
-            L += [f"s_add_u32 s38, s38, {t * 256 * BLOCK}", "s_addc_u32 s39, s39, 0"]
+        if inl:  # the products of a fixed coefficient per row, no call
+            L += block_body(0x53 + i, i, rel)
+            continue
+        L += [f"s_add_u32 s38, s36, s{44 + i}", "s_addc_u32 s39, s37, 0"]  # offsets hold c * this stride
         L.append("s_swappc_b64 s[40:41], s[38:39]")
     L += ["s_sub_u32 s43, s43, 1", "s_cmp_eq_u32 s43, 0", "s_cbranch_scc0 1b"]
-    if mode == "rel1":
+    if rel:
         L.append("s_set_gpr_idx_off")
     return "\\n\\t".join(L)
 
 
 def gen(path):
     clob = ", ".join(f'"v{r}"' for r in range(192)) + ", " + ", ".join(f'"s{r}"' for r in range(36, 56))
-    modes = ["rel1", "abs8", "abs1"]
+    modes = list(MODES)
     src = ['#include <hip/hip_runtime.h>', '#include <cstdio>', '#include <vector>', '#include <cstdint>']
     movs = "\n".join(f'                 "v_mov_b32 v{r}, v{r % 4}\\n"' for r in range(4, 192))
     for mi, mode in enumerate(modes):
@@ -105,6 +132,7 @@ __global__ __launch_bounds__(256) void k_{mode}(unsigned long long *out, int rep
                  ::: {clob});
     const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    offs += {mi} * 64 * 8 * 128;  // this mode's offsets (c * its block stride)
     asm volatile("{prog}" : : [offs] "s"(offs + (blockIdx.x % 64) * 8 * 128), [reps] "s"(reps) : {clob}, "m0", "scc", "memory");
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
@@ -148,15 +176,20 @@ int main() {
     (void)hipGetDeviceProperties(&prop, 0);
     const int cus = prop.multiProcessorCount;
     unsigned long long *d;
-    uint32_t *offs, *seed;
+    uint32_t *offs;
     (void)hipMalloc(&d, size_t(cus) * 4 * 4 * 4 * sizeof(unsigned long long));
-    (void)hipMalloc(&offs, 64 * 8 * 128 * sizeof(uint32_t));
+    uint32_t *seed;
+    const int nmodes = NMODES;
+    const int strides[NMODES] = {STRIDES};
+    const char *names[NMODES] = {NAMES};
+    (void)hipMalloc(&offs, size_t(nmodes) * 64 * 8 * 128 * sizeof(uint32_t));
     (void)hipMalloc(&seed, 4096 * 4 * sizeof(uint32_t));
-    std::vector<uint32_t> h(64 * 8 * 128), hs(4096 * 4);
+    std::vector<uint32_t> h(size_t(nmodes) * 64 * 8 * 128), hs(4096 * 4);
     uint32_t x = 12345;
-    for (auto &v : h) {
+    for (size_t i = 0; i < 64 * 8 * 128; ++i) {
         x = x * 1103515245u + 12345u;
-        v = ((x >> 16) & 255u) * ''' + str(BLOCK) + '''u;
+        const uint32_t c = (x >> 16) & 255u;
+        for (int mm = 0; mm < nmodes; ++mm) h[size_t(mm) * 64 * 8 * 128 + i] = c * uint32_t(strides[mm]);
     }
     for (auto &v : hs) {
         x = x * 1103515245u + 12345u;
@@ -165,13 +198,17 @@ int main() {
     (void)hipMemcpy(offs, h.data(), h.size() * 4, hipMemcpyHostToDevice);
     (void)hipMemcpy(seed, hs.data(), hs.size() * 4, hipMemcpyHostToDevice);
     for (int W : {2, 4}) {
-        run("rel1: one table, relative accumulators (product form)", k_rel1, W, d, offs, seed, cus);
-        run("abs8: eight tables (one per row slot), absolute operands", k_abs8, W, d, offs, seed, cus);
-        run("abs1: one table, absolute operands, slot 0 only", k_abs1, W, d, offs, seed, cus);
+RUNS
     }
     return 0;
 }
 ''')
+    text = "\n".join(src)
+    text = text.replace("NMODES", str(len(modes)))
+    text = text.replace("{STRIDES}", "{" + ", ".join(str(block_stride(m)) for m in modes) + "}")
+    text = text.replace("{NAMES}", "{" + ", ".join(f'"{m}"' for m in modes) + "}")
+    text = text.replace("RUNS", "\n".join(f"        run(names[{i}], k_{m}, W, d, offs, seed, cus);" for i, m in enumerate(modes)))
+    src = [text]
     os.makedirs(os.path.dirname(path), exist_ok=True)
     with open(path, "w") as f:
         f.write("\n".join(src))
