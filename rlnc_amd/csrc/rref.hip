@@ -1206,10 +1206,12 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
             __syncthreads();
         }
         BPROF(1);  // step 1 (with the block's initial rows)
-        // 2. the block's rows among themselves (every wave, registers; lane groups hold identical copies).  No
+        // 2. the block's rows among themselves (every wave redundantly, registers, lane = dword; lane groups hold identical copies: wave 0 alone with the
+        // rows passed through LDS measured equal, profiles/r02_elim_ab.txt).  No
         // branch inside a piece's forward or backward products: their table reads are issued together.
         uint32_t y[B];
         int c = b;
+        {
 #pragma unroll
         for (int t = 0; t < B; ++t) y[t] = t < b ? X[t * D + w] : 0u;
 #pragma unroll
@@ -1253,6 +1255,7 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
                                      xor3(__builtin_amdgcn_perm(b4[s2].w, b4[s2].z, e1), __builtin_amdgcn_perm(b2[s2], b2[s2], e2), 0u));
                 }
             }
+        }
         }
         BPROF(2);
         // 3. rows j < r: R_j ^= Σ_{t<c} R_j[r+t]·y_t; then y_t become rows r..r+c-1

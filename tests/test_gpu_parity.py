@@ -385,7 +385,8 @@ def test_decode_batch_vs_oracle_sequences(ctx, path, k, m, L, sparsity, dep):
 
 
 @pytest.mark.parametrize("k,m,sparsity,dep", [(32, 48, 0.5, 0.05), (64, 64, 0.3, 0.02), (16, 40, 0.6, 0.1),
-                                               (128, 128, 0.05, 0.0), (48, 64, 0.8, 0.0), (96, 100, 0.2, 0.05)])
+                                               (128, 128, 0.05, 0.0), (48, 64, 0.8, 0.0), (96, 100, 0.2, 0.05),
+                                               (32, 20, 0.0, 0.0), (64, 40, 0.3, 0.1), (128, 100, 0.5, 0.0)])
 def test_decode_blocked_path_stress(ctx, k, m, sparsity, dep):
     """The blocked elimination (path 5) against the oracle on 64 objects per shape: sparse coefficients drive the
     matrix in and out of the clean state (zero pivots, kept dirty rows, prefix re-extension, the many-dirty-rows

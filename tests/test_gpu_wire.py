@@ -155,10 +155,12 @@ def test_encode_ragged_vs_oracle(ctx, orc):
         assert np.array_equal(host(t.contiguous()), w)
 
 
+@pytest.mark.parametrize("window", [1, 2])
 @pytest.mark.parametrize("pinned", [False, True])
-def test_host_stream_encode_decode_vs_oracle(ctx, orc, pinned):
+def test_host_stream_encode_decode_vs_oracle(ctx, orc, pinned, window):
     """Pieces start and end in host memory: encode n coded pieces per object, decode the first m back; windows of
-    2 objects over 7 objects (three slots in flight), against the oracle and the device-resident batch."""
+    1 or 2 objects over 7 objects (4-7 windows through 3 slots: every slot refilled behind its previous kernel and
+    device-to-host copy), against the oracle and the device-resident batch."""
     import torch
 
     from rlnc_amd import batch
@@ -179,7 +181,7 @@ def test_host_stream_encode_decode_vs_oracle(ctx, orc, pinned):
     co = buf((nobj, n, k), co_np)
     pieces = buf((nobj, n, k + L), 0)
     p = lambda t: C.c_void_p(t.data_ptr())
-    assert ctx.lib.rlnc_encode_host_stream(ctx.h, p(src), k, L, nobj, p(co), n, p(pieces), 2) == 0
+    assert ctx.lib.rlnc_encode_host_stream(ctx.h, p(src), k, L, nobj, p(co), n, p(pieces), window) == 0
     hp = pieces.numpy()
     for o in range(nobj):
         assert np.array_equal(hp[o], orc.encode(src.numpy()[o], co_np[o])), o
@@ -190,7 +192,7 @@ def test_host_stream_encode_decode_vs_oracle(ctx, orc, pinned):
     assert ctx.lib.rlnc_decode_host_stream(ctx.h, p(pieces), n * (k + L), k, L, m, nobj, p(decoded),
                                            ps.ctypes.data_as(C.POINTER(C.c_int32)),
                                            os_.ctypes.data_as(C.POINTER(C.c_int32)),
-                                           dl.ctypes.data_as(C.POINTER(C.c_uint64)), 2) == 0
+                                           dl.ctypes.data_as(C.POINTER(C.c_uint64)), window) == 0
     hd = decoded.numpy()
     for o in range(nobj):
         od = OracleDecoder(L, k)
