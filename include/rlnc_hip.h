@@ -286,10 +286,12 @@ int rlnc_encode_ragged(rlnc_context *ctx, const rlnc_object_desc *objs, size_t c
 
 /* ---- host-resident pieces (a socket or a file) ---------------------------------------------
  * The batch API above for host buffers: objects stream through the device in windows of `window` objects (0 =
- * automatic, >= 64 MiB of input per window), three pipeline slots with their own streams so that window w+1's
- * host-to-device copy, window w's encode/decode and window w-1's device-to-host copy overlap.  Pinned host buffers
- * (hipHostMalloc / hipHostRegister) are copied by DMA directly; pageable ones are staged through pinned buffers by
- * host threads.  Same results as the device-resident calls (they run them).  Synchronous. */
+ * automatic, >= 32 MiB of input per window) as a three-stage pipeline on three streams (host-to-device copies, the
+ * encode/decode on the context's stream, device-to-host copies; windows rotate over three slots of device buffers,
+ * ordered by events), so that window w+1's copy in, window w's encode/decode and window w-1's copy out overlap.
+ * Pinned host buffers (hipHostMalloc / hipHostRegister) are copied by DMA directly; pageable ones are staged through
+ * pinned buffers by host threads.  Same results as the device-resident calls (they run them).  Synchronous; like the
+ * batch calls, one caller thread per context at a time (the slot buffers and copy streams belong to the context). */
 /* src [obj][k][L], coeffs [obj][n][k] → pieces [obj][n][k+L] (rlnc_encode_batch). */
 int rlnc_encode_host_stream(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t num_objects,
                             const uint8_t *coeffs, size_t n, uint8_t *pieces, size_t window);
