@@ -26,11 +26,39 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def bind_to_gpu_node(dev=0):
+    """Pin this process's threads to the CPUs of the GPU's NUMA node (the pinned host buffers are then first-touched
+    there, so PCIe traffic does not cross the socket interconnect).  Returns the node, or None if unknown."""
+    import torch
+
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        bus = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+    except Exception:
+        return None
+    try:
+        node = int(open(f"/sys/bus/pci/devices/{bus.lower()}/numa_node").read())
+        if node < 0:
+            return None
+        cpus = set()
+        for part in open(f"/sys/devices/system/node/node{node}/cpulist").read().strip().split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        cpus &= os.sched_getaffinity(0)
+        if not cpus:
+            return None
+        os.sched_setaffinity(0, cpus)
+        return node
+    except OSError:
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--objects", type=int, default=16)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--window", type=int, default=0, help="objects per pipeline window (0 = library default)")
+    ap.add_argument("--no-numa-bind", action="store_true", help="do not pin the process to the GPU's NUMA node")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -39,12 +67,14 @@ def main():
     import rlnc_amd
 
     k, L, n, m, B = 32, 1 << 20, 64, 32, args.objects
+    node = None if args.no_numa_bind else bind_to_gpu_node(0)
     ctx = rlnc_amd.Context(0)
     lib = ctx.lib
     rng = np.random.default_rng(1)
     out = {"metric": "host-resident RLNC encode+decode GiB/s (library pipeline, host buffers in and out), "
                      "k=32 x 1 MiB", "unit": "GiB/s", "objects": B,
-           "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)")}
+           "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)"),
+           "numa_node_bound": node, "cpus": len(os.sched_getaffinity(0))}
     for mode in ("pinned", "pageable"):
         pin = mode == "pinned"
 
