@@ -31,8 +31,10 @@ is preset once the prologue has checked that the block table does not straddle a
 copy with the carry runs), and rows past n_out have c = 0, whose block returns at once.
 
 Shared-combination program (RLNC_BSJ_ASM_W4S, variant 7) calls absolute block addresses: the offset kernel writes
-base + c * BLOCK_BYTES (64-bit; the base is read once per device by a probe launch of this program, which stores
-it and exits), two s_load_dwordx16 buffers of 8 addresses, so a call is s_mov m0 + s_swappc_b64 + s_setpc_b64.
+base + offset of block c (64-bit; the base is read once per device by a probe launch of this program, which stores
+it and exits), two s_load_dwordx16 buffers of 8 addresses, so a call is an M0 step (s_add_u32 m0, m0, 16) +
+s_swappc_b64 + s_setpc_b64.  Its blocks are packed (--pack): the accumulator is SRC0 (GPR-index mode SRC0 + DST),
+so a product whose low or high half selects nothing is a 4-byte v_xor_b32 instead of an XOR3 with a zero operand.
 With 4 waves on one column block, wave w builds
 only set w = (group w >> 1, half w & 1) of the plane combinations -- half of one group's transpose + 11 XORs
 instead of two full transposes + 44 XORs -- and the four sets (4 KiB each) are exchanged through two 16 KiB
@@ -218,6 +220,52 @@ def blocks(lines):
 FAST = True  # the loop being generated: True = high half of every block address preset (no carry, checked)
 
 
+# The shared programs step M0 by 16 between calls (a 4-byte SALU) instead of moving an 8-byte literal (--no-m0step);
+# with --pack (default) the two are worth -0.3 % encode and -1.1 % decode time, 5 interleaved passes
+# (profiles/r02_bsj_thread_ab.txt)
+M0STEP = True
+
+
+# --pack: the shared programs' blocks with the accumulator as SRC0 (GPR-index mode SRC0 + DST), so that a product
+# whose low or high half selects nothing is a 4-byte VOP2 v_xor_b32 instead of an 8-byte XOR3 with a zero operand;
+# blocks packed at their own size (XOR3s first, 8-byte grid), the offset kernel reads the block offsets from a table
+PACK = True
+
+
+def idx_mode():
+    return "gpr_idx(SRC0,DST)" if PACK else "gpr_idx(SRC2,DST)"
+
+
+def m0_slot(i):
+    """M0 = row slot i's GPR-index base (after slot i - 1's call when stepping)."""
+    if M0STEP and i:
+        return "s_add_u32 m0, m0, 16"
+    return f"s_mov_b32 m0, {hex((0x9000 if PACK else 0xC000) | (16 * i))}"
+
+
+def blocks_packed(lines):
+    """The 256 blocks at their own sizes; returns their byte offsets from the table start."""
+    offs, pos = [], 0
+    for c in range(256):
+        lo, hi = block_indices(c)
+        v3, v2 = [], []
+        for g in range(2):
+            for o in range(8):
+                a = ACC(0, g, o)
+                if c == 0 or (lo[o] == 0 and hi[o] == 0):
+                    continue
+                if lo[o] and hi[o]:
+                    v3.append(f"v_bitop3_b32 v{a}, v{a}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])} bitop3:0x96")
+                else:
+                    v2.append(f"v_xor_b32 v{a}, v{a}, v{G(g, 0, lo[o]) if lo[o] else G(g, 1, hi[o])}")
+        size = 8 * len(v3) + 4 * len(v2) + 4
+        pad = (-size) % 8
+        offs.append(pos)
+        lines += v3 + v2 + [f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]"] + ["s_nop 0"] * (pad // 4)
+        pos += size + pad
+    return offs
+
+
 def call(L, cur, i):
     """Row i's product of the current source: M0 = its accumulator slot, then the call into block c (whose
     offset c * BLOCK_BYTES is s[cur + i]).  Rows past n_out have c = 0, whose block returns at once.  The fast
@@ -394,7 +442,7 @@ def body_s(L, j, cons=False):
         f"s_load_dwordx16 s[{nxt}:{nxt + 15}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
         f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
         f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
-        "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)",
+        f"s_set_gpr_idx_on 0, {idx_mode()}",
     ]
     for i in range(NT):
         if "sinline" in DIAG:  # timing only: a fixed coefficient's products inline (relative), no call
@@ -407,8 +455,7 @@ def body_s(L, j, cons=False):
             L.append(f"s_setprio {PRIO_AT[1]}")
         # row i: M0 = its accumulator slot, then the call to the absolute address of block c (rows past
         # n_out have c = 0, whose block returns at once)
-        L += [f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}",
-              f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{cur + 2 * i}:{cur + 2 * i + 1}]"]
+        L += [m0_slot(i), f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{cur + 2 * i}:{cur + 2 * i + 1}]"]
     L.append("s_set_gpr_idx_off")
 
 
@@ -484,9 +531,17 @@ def program_shared_body(cons=False):
     if ALIGN:
         L.append(f".p2align {ALIGN}")
     L.append("9:")
-    blocks(L)
+    global SOFFS
+    if PACK:
+        SOFFS = blocks_packed(L)
+    else:
+        blocks(L)
+        SOFFS = None
     L.append("8:")
     return L
+
+
+SOFFS = None  # byte offsets of the shared programs' packed blocks (--pack)
 
 
 # 8-wave program: one workgroup per CU leaves LDS for SLOTS8 ring slots and CSLOTS8 = 2 BAR8 set slots, so the
@@ -551,13 +606,12 @@ def body_s8(L, j):
         f"s_load_dwordx16 s[{nxt}:{nxt + 15}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
         f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
         f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
-        "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)",
+        f"s_set_gpr_idx_on 0, {idx_mode()}",
     ]
     for i in range(NT):
         if PRIO8 is not None and i == PRIO8[0]:
             L.append(f"s_setprio {PRIO8[1]}")
-        L += [f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}",
-              f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{cur + 2 * i}:{cur + 2 * i + 1}]"]
+        L += [m0_slot(i), f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{cur + 2 * i}:{cur + 2 * i + 1}]"]
     L.append("s_set_gpr_idx_off")
 
 
@@ -679,12 +733,18 @@ def main():
     ap.add_argument("--align", type=int, default=DEFAULT_ALIGN, help="log2 alignment of the block table")
     ap.add_argument("--bar8", type=int, default=3, choices=(2, 3), help="8-wave program: a barrier every N rows")
     ap.add_argument("--prio8", default="off", help="K,L: 8-wave program's calls K.. of each row at s_setprio L")
+    ap.add_argument("--no-m0step", action="store_true", help="shared programs: M0 moved as a literal per call")
+    ap.add_argument("--no-pack", action="store_true", help="shared programs: fixed-stride XOR3-only blocks")
     ap.add_argument("--prio", default="", help="K,L: shared program's calls K.. of each row at s_setprio L")
     args = ap.parse_args()
     global PRIO_AT
     if args.prio:
         PRIO_AT = None if args.prio == "off" else tuple(int(x) for x in args.prio.split(","))
     DIAG.update(x for x in args.diag.split(",") if x)
+    global M0STEP
+    M0STEP = not args.no_m0step
+    global PACK
+    PACK = not args.no_pack
     set_bar8(args.bar8)
     global PRIO8
     PRIO8 = None if args.prio8 == "off" else tuple(int(x) for x in args.prio8.split(","))
@@ -712,6 +772,8 @@ def main():
         body_txt = "\\n\\t".join(program_shared(cons=True))
         f.write(f'#define RLNC_BSJ_ASM_W8S "{body_txt}"\n')
         f.write(f"#define RLNC_BSJ_SLOTS8 {SLOTS8}\n")
+        if SOFFS is not None:  # block offsets of the shared programs' packed table (bsj_offset_kernel<true>)
+            f.write("#define RLNC_BSJ_SOFFSETS {" + ", ".join(str(x) for x in SOFFS) + "}\n")
         f.write(f"#define RLNC_BSJ_CSET_BYTES8 {CSLOTS8 * CS_SLOT}\n")
         f.write(f"#define RLNC_BSJ_CSET_BYTES {2 * CS_SLOT}\n")
         f.write(f"#define RLNC_BSJ_CLOBBER_V {clob_v}\n")

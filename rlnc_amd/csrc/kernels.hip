@@ -913,8 +913,13 @@ hipError_t launch_bs(const MatmulParams &p, hipStream_t s, void *scratch, size_t
 constexpr int kBsjWaveRows = RLNC_BSJ_NT;  // output rows per wave; a workgroup of W waves = 8 W rows
 constexpr int kBsjColBlock = 4096;          // 64 lanes × 64 B, shared by the W waves
 
+#ifdef RLNC_BSJ_SOFFSETS  // the shared programs' blocks packed at their own sizes (gen_bsjump.py --pack)
+__constant__ uint32_t kBsjSharedOff[256] = RLNC_BSJ_SOFFSETS;
+#endif
+
 // stream[obj][row tile][j][row in tile] = c · RLNC_BSJ_BLOCK_BYTES (c = 0 for rows past n_out); ABS: the
-// block's absolute address base + c · RLNC_BSJ_BLOCK_BYTES (64-bit, the shared-set program calls it directly)
+// block's absolute address (64-bit, the shared-set programs call it directly): base + kBsjSharedOff[c] for their
+// packed table, base + c · RLNC_BSJ_BLOCK_BYTES for a fixed-stride one (gen_bsjump.py --no-pack)
 template <bool ABS>
 __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, int64_t coef_obj, int64_t coef_row,
                                                          int n_out, int n_in, int row_tiles, int tile_rows,
@@ -929,7 +934,11 @@ __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, in
     const int row = rt * tile_rows + i;
     const uint32_t c = row < n_out ? coef[int64_t(obj) * coef_obj + int64_t(row) * coef_row + j] : 0u;
     if constexpr (ABS)
+#ifdef RLNC_BSJ_SOFFSETS
+        static_cast<uint64_t *>(stream)[int64_t(obj) * per_obj + e] = base + kBsjSharedOff[c];
+#else
         static_cast<uint64_t *>(stream)[int64_t(obj) * per_obj + e] = base + uint64_t(c) * RLNC_BSJ_BLOCK_BYTES;
+#endif
     else
         static_cast<uint32_t *>(stream)[int64_t(obj) * per_obj + e] = c * uint32_t(RLNC_BSJ_BLOCK_BYTES);
 }

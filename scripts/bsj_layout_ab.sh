@@ -9,7 +9,7 @@ OUT=gpurun_out; mkdir -p $OUT
 cp rlnc_amd/librlnc_hip.so /tmp/librlnc_hip.base.so
 : > $OUT/bsj_layout_ab.jsonl
 rc=0
-for pass in 1 2; do
+for pass in $(seq 1 ${PASSES:-2}); do
   for v in base ${VARIANTS:-s256a8 s192a6 s136a3}; do
     if [ $v = base ]; then cp /tmp/librlnc_hip.base.so rlnc_amd/librlnc_hip.so; else cp build/var/$v/librlnc_hip.so rlnc_amd/librlnc_hip.so; fi
     if [ $pass = 1 ]; then
