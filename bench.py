@@ -61,13 +61,14 @@ def decode_counter(k: int, L: int) -> int:
 
 
 VARIANTS = ["perm", "nibble", "perm3", "wide2", "wide4", "bitsliced", "bitsliced-jump", "bitsliced-jump-shared",
-            "bitsliced-jump-shared-8w"]
+            "bitsliced-jump-shared-8w", "bitsliced-jump-run"]
 KERNELS = {"perm": "gf_matmul_perm_kernel", "nibble": "gf_matmul_nibble_kernel", "perm3": "gf_matmul_perm3_kernel",
            "wide2": "gf_matmul_wide_kernel", "wide4": "gf_matmul_wide_kernel",
            "bitsliced": "bs_index_kernel + gf_matmul_bs_kernel",
            "bitsliced-jump": "bsj_offset_kernel + gf_matmul_bsj_kernel",
            "bitsliced-jump-shared": "bsj_offset_kernel + gf_matmul_bsj_kernel<4, true>",
-           "bitsliced-jump-shared-8w": "bsj_offset_kernel + gf_matmul_bsj_kernel<8, true>"}
+           "bitsliced-jump-shared-8w": "bsj_offset_kernel + gf_matmul_bsj_kernel<8, true>",
+           "bitsliced-jump-run": "bsj_offset_kernel + gf_matmul_bsj_kernel<8, true, true>"}
 
 
 def pmc_traffic(variant: str, B: int, k: int, L: int, n: int):
@@ -311,7 +312,7 @@ def parse_args(argv=None):
     ap.add_argument("--coded", type=int, default=None)
     ap.add_argument("--decode-from", type=int, default=None)
     ap.add_argument("--chunk", type=int, default=None, help="objects per launch (config5: 512)")
-    ap.add_argument("--variant", type=int, default=8, help="matmul kernel variant: 8 as 7 with 64-row tiles of 8 waves above 32 output rows and a barrier every third row (default), 7 bit-sliced, one code block per coefficient, combinations shared through LDS, 6 the same without sharing, 5 bit-sliced relative XOR, 0 perm, 1 nibble-LDS, 2 perm3, 3/4 wide")
+    ap.add_argument("--variant", type=int, default=8, help="matmul kernel variant: 8 as 7 with 64-row tiles of 8 waves above 32 output rows and a barrier every third row (default), 9 as 8 with column runs (a workgroup walks up to 8 column blocks, one prologue per run), 7 bit-sliced, one code block per coefficient, combinations shared through LDS, 6 the same without sharing, 5 bit-sliced relative XOR, 0 perm, 1 nibble-LDS, 2 perm3, 3/4 wide")
     ap.add_argument("--tile-rows", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

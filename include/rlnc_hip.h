@@ -123,8 +123,15 @@ int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc);
  *   8 = bitsliced-jump-shared-8w  as 7; above 32 output rows, 64-row tiles of 8 waves (one workgroup per CU):
  *                  waves 0-3 stage the source and build the combinations three rows ahead, waves 4-7 only
  *                  read them and call; a barrier every third row -- the default
+ *   9 = bitsliced-jump-run  as 8, with column runs: above 32 output rows a workgroup walks up to 8 consecutive
+ *                  4 KiB column blocks of one object, its source-row stream (DMA, staging, combinations, block
+ *                  addresses) unbroken across them, so only a run's first block pays the prologue (5 % faster
+ *                  for an isolated large launch, not beside other launches)
  * max_tile_rows caps the output rows per launch/workgroup (0 = automatic, else 1/2/4/8/16/32). */
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows);
+/* Column blocks per workgroup of variant 9 (0 = automatic: enough runs for >= 4 workgroups per CU, at most 8;
+ * else 1..64).  A tuning and test knob; results are bit-identical for every value. */
+int rlnc_set_column_run(rlnc_context *ctx, int col_run);
 /* Where rlnc_decode_batch runs the coefficient elimination: 0 = auto (device when it fits LDS, default),
  * 1 = host threads, 2 = device, 3 = device with the clean-state steps on LDS instead of registers, 4 = device
  * with the clean-state steps on one wave's registers, 5 = device, blocked clean run (up to 16 pieces per step,

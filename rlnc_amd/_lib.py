@@ -57,6 +57,7 @@ _SIGS = {
     "rlnc_gf256_mul_vec_by_scalar_then_add_into_vec": (C.c_int, [vp, vp, vp, C.c_size_t, C.c_uint8]),
     "rlnc_gf256_matmul": (C.c_int, [vp, C.POINTER(MatmulDesc)]),
     "rlnc_set_kernel_variant": (C.c_int, [vp, C.c_int, C.c_int]),
+    "rlnc_set_column_run": (C.c_int, [vp, C.c_int]),
     "rlnc_set_decode_path": (C.c_int, [vp, C.c_int]),
     "rlnc_encoder_new": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.POINTER(vp)]),
     "rlnc_encoder_without_padding": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.POINTER(vp)]),

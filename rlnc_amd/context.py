@@ -57,8 +57,13 @@ class Context:
         combinations built once per workgroup and shared through LDS, 6 = the same without sharing,
         5 = bit-sliced with register-indexed XORs, 0 = perm, 1 = nibble (the reference's 4-bit tables,
         ablation), 2 = perm3, 3/4 = wide2/wide4, 8 = as 7 with 64-row tiles of 8 waves above 32 output rows
-        (waves 4-7 only read the shared combinations; a barrier every third row; the default).  All are bit-identical."""
+        (waves 4-7 only read the shared combinations; a barrier every third row; the default), 9 = as 8 with
+        column runs (a workgroup walks up to 8 column blocks, one prologue per run).  All are bit-identical."""
         check(self.lib.rlnc_set_kernel_variant(self.h, int(variant), int(max_tile_rows)), self.lib)
+
+    def set_column_run(self, col_run: int = 0):
+        """Column blocks per workgroup of variant 9 (0 = automatic)."""
+        check(self.lib.rlnc_set_column_run(self.h, int(col_run)), self.lib)
 
 
 def default_context(device: int = 0) -> Context:

@@ -120,8 +120,11 @@ struct rlnc_context {
     int device = 0;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
+    // variant 9 (column runs) is 5 % faster for an isolated encode launch but not in the bench's pipelined step,
+    // whose encode and decode launches share the CUs better with short workgroups (profiles/r02_run_ab.txt)
     rlnc::MatmulVariant variant = rlnc::MatmulVariant::BitSlicedJumpShared8;
     int max_tile_rows = 0;
+    int col_run = 0;  // column blocks per workgroup of variant 9 (0 = chosen per launch; rlnc_set_column_run)
     int decode_path = 0;  // 0 auto (device when it fits LDS), 1 host elimination, 2 device elimination,
                           // 3 device elimination with the clean state on LDS, 4 ... on one wave's
                           // registers, 5 blocked clean run, 6 round-1 multi-wave registers (A/B)
@@ -230,8 +233,9 @@ struct rlnc_context {
         return launch(p, s, idx, batch);
     }
     int matmul(const rlnc::MatmulParams &p) { return matmul(p, stream, ws_idx, true); }
-    int launch(const rlnc::MatmulParams &p, hipStream_t s, DevBuf &idx, bool batch) {
+    int launch(rlnc::MatmulParams p, hipStream_t s, DevBuf &idx, bool batch) {
         const rlnc::MatmulVariant v = variant;
+        p.col_run = col_run;
         const size_t need = rlnc::matmul_scratch_bytes(p, v);
         if (need)
             if (int st = batch ? grow(idx, need) : idx.ensure(need)) return st;

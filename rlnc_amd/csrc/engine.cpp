@@ -239,11 +239,18 @@ int rlnc_set_decode_path(rlnc_context *ctx, int path) {
 
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows) {
     CHECK_ARG(ctx != nullptr);
-    CHECK_ARG(variant >= 0 && variant <= 8);
+    CHECK_ARG(variant >= 0 && variant <= 9);
     CHECK_ARG(max_tile_rows == 0 || max_tile_rows == 1 || max_tile_rows == 2 || max_tile_rows == 4 ||
               max_tile_rows == 8 || max_tile_rows == 16 || max_tile_rows == 32);
     ctx->variant = static_cast<rlnc::MatmulVariant>(variant);
     ctx->max_tile_rows = max_tile_rows;
+    return RLNC_OK;
+}
+
+int rlnc_set_column_run(rlnc_context *ctx, int col_run) {
+    CHECK_ARG(ctx != nullptr);
+    CHECK_ARG(col_run >= 0 && col_run <= 64);
+    ctx->col_run = col_run;
     return RLNC_OK;
 }
 

@@ -101,7 +101,15 @@ S_ADDR = (36, 52)
 SHARED_SGPRS = dict(S_SRC=68, S_IDX=70, S_DST=72, S_BASE=74, S_TGT=76, S_RET=78, S_INROW=80, S_OUTROW=81, S_CNT=82,
                     S_ROWS=83, S_T0=84, S_LDSW=85, S_NDMA=86, S_H=87)
 S_CONS = 88  # 8-wave program: 1 for the consumer waves 4-7
-LAST_VGPR_ALL, LAST_SGPR_ALL = 243, 88
+# column-run programs (--run, variant 9): one workgroup walks `tiles` consecutive 4 KiB column blocks of one
+# (object, row tile); the source-row stream runs on across the tile boundaries (DMA, staging, set building and the
+# block addresses continue into the next tile's rows), so a tile's prologue costs nothing but its epilogue
+S_IDXM = 74  # 64-bit: the wave's block-address stream start minus one row (S_BASE is unused by the 8-wave program)
+S_DTL, S_SRCT, S_DST0, S_TL, S_POS, S_NIN = 89, 90, 92, 94, 95, 96
+# Measured and not kept (profiles/r02_run_ab.txt): builders waiting on vmcnt at the barrier rows only, with
+# vmcnt(1 + 32) for the two rows after a tile switch (so the next rows' DMA waits do not include the epilogue's
+# stores, which retire in issue order ahead of them): 1.4 % slower than a vmcnt(1) wait in every row.
+LAST_VGPR_ALL, LAST_SGPR_ALL = 243, 96
 
 DIAG = set()
 # The shared program raises the wave priority (s_setprio) for the calls from PRIO_AT[0] on and drops it after
@@ -383,6 +391,32 @@ def advance_s(L):
     ]
 
 
+def advance_run(L):
+    """advance_s for the column-run program: past the tile's last source row the DMA stream moves on to row 0 of
+    the next column block (S_SRCT + 4 KiB) while the workgroup has one (S_DTL counts the tiles the DMA stream
+    has still to enter), else stays (the re-read is harmless, always in bounds)."""
+    L += [
+        f"s_cmp_gt_u32 s{S_NDMA}, 0",
+        "s_cbranch_scc0 30f",
+        f"s_sub_u32 s{S_NDMA}, s{S_NDMA}, 1",
+        f"s_add_u32 s{S_SRC}, s{S_SRC}, s{S_INROW}",
+        f"s_addc_u32 s{S_SRC + 1}, s{S_SRC + 1}, 0",
+        "s_branch 31f",
+        "30:",
+        f"s_cmp_gt_u32 s{S_DTL}, 1",
+        "s_cbranch_scc0 31f",
+        f"s_sub_u32 s{S_DTL}, s{S_DTL}, 1",
+        f"s_add_u32 s{S_SRCT}, s{S_SRCT}, 4096",
+        f"s_addc_u32 s{S_SRCT + 1}, s{S_SRCT + 1}, 0",
+        f"s_mov_b64 s[{S_SRC}:{S_SRC + 1}], s[{S_SRCT}:{S_SRCT + 1}]",
+        f"s_sub_u32 s{S_NDMA}, s{S_NIN}, 1",
+        "31:",
+    ]
+
+
+RUN = False  # the 8-wave program being generated is the column-run form
+
+
 def own_set(L, rb, cslot):
     """Set (g, h) of the row staged in RB[rb]: planes 4h..4h+3 by the half transpose, the 11 composite
     entries by VOP2 XORs, then 4 ds_write_b128 to set slot `cslot` (entry 0 is the zero register)."""
@@ -575,7 +609,10 @@ def body_s8(L, j):
     row j + BAR8 + 1, the DMA of row j + DMA8 and the own set of row j + BAR8; then row j's products.  Barrier
     when j % BAR8 == 0: it orders the set writes of rows j .. j + BAR8 - 1 before their reads, the ring landing of
     rows <= j + 2 BAR8 before their staging reads and every read of a slot before its reuse."""
-    L.append("s_waitcnt vmcnt(1) lgkmcnt(0)")  # rows <= j+DMA8-2 landed; own LDS ops + addresses done
+    if RUN:  # consumers have no loads in flight, only the last tile's stores: never wait on those
+        L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 24f", "s_waitcnt vmcnt(1)", "24:", "s_waitcnt lgkmcnt(0)"]
+    else:
+        L.append("s_waitcnt vmcnt(1) lgkmcnt(0)")  # rows <= j+DMA8-2 landed; own LDS ops + addresses done
     if j % BAR8 == 0:
         L.append("s_barrier")
     L.append(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
@@ -593,7 +630,7 @@ def body_s8(L, j):
     for hh in range(2):
         r = RB(nx % 2, 4 * hh)
         L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{(nx % SLOTS8) * 4096 + hh * 1024}")
-    advance_s(L)
+    advance_run(L) if RUN else advance_s(L)
     L += [f"s_add_u32 m0, s{S_LDSW}, {((j + DMA8) % SLOTS8) * 4096}", "s_nop 0",
           "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)]  # row j + DMA8
     own_set(L, (j + BAR8) % 2, (j + BAR8) % CSLOTS8)  # row j + BAR8's set
@@ -602,6 +639,9 @@ def body_s8(L, j):
     L += ["s_waitcnt lgkmcnt(6)",  # the 16 set reads (2 staging reads + 4 set writes may fly)
           "s_branch 21f", "20:", "s_waitcnt lgkmcnt(0)", "21:"]
     cur, nxt = S_ADDR[j % 2], S_ADDR[(j + 1) % 2]
+    if RUN:  # row j is the tile's last: the next row's addresses are row 0's (the next column block, same rows)
+        L += [f"s_cmp_eq_u32 s{S_CNT}, 0",
+              f"s_cselect_b64 s[{S_IDX}:{S_IDX + 1}], s[{S_IDXM}:{S_IDXM + 1}], s[{S_IDX}:{S_IDX + 1}]"]
     L += [
         f"s_load_dwordx16 s[{nxt}:{nxt + 15}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
         f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
@@ -616,7 +656,14 @@ def body_s8(L, j):
 
 
 def program_shared8():
-    L = [
+    L = []
+    if RUN:
+        L += [f"s_mov_b64 s[{S_SRCT}:{S_SRCT + 1}], %[src]",
+              f"s_mov_b64 s[{S_DST0}:{S_DST0 + 1}], %[dst]",
+              f"s_mov_b32 s{S_TL}, %[tiles]",
+              f"s_mov_b32 s{S_DTL}, %[tiles]",
+              f"s_mov_b32 s{S_NIN}, %[n_in]"]
+    L += [
         f"s_mov_b64 s[{S_SRC}:{S_SRC + 1}], %[src]",
         f"s_mov_b64 s[{S_IDX}:{S_IDX + 1}], %[idx]",
         f"s_mov_b64 s[{S_DST}:{S_DST + 1}], %[dst]",
@@ -627,6 +674,10 @@ def program_shared8():
         f"s_mov_b32 s{S_H}, %[half]",
         f"s_mov_b32 s{S_ROWS}, %[rows]",
         f"s_mov_b32 s{S_CONS}, %[cons]",
+    ]
+    if RUN:  # the wave's block-address stream start minus one row
+        L += [f"s_sub_u32 s{S_IDXM}, s{S_IDX}, {STREAM_J_BYTES}", f"s_subb_u32 s{S_IDXM + 1}, s{S_IDX + 1}, 0"]
+    L += [
         f"v_mov_b32 v{V_MASK[0]}, 0xaaaaaaaa",
         f"v_mov_b32 v{V_MASK[1]}, 0xcccccccc",
         f"v_mov_b32 v{V_MASK[2]}, 0xf0f0f0f0",
@@ -637,7 +688,7 @@ def program_shared8():
     dmai = "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)
     for slot in range(DMA8):  # builders: rows 0 .. DMA8 - 1 (clamped to the last row) into ring slots
         if slot:
-            advance_s(L)
+            advance_run(L) if RUN else advance_s(L)
         L += [f"s_add_u32 m0, s{S_LDSW}, {slot * 4096}", "s_nop 0", dmai]
     L.append("22:")
     L.append(f"s_load_dwordx16 s[{S_ADDR[0]}:{S_ADDR[0] + 15}], s[{S_IDX}:{S_IDX + 1}], 0")
@@ -660,11 +711,40 @@ def program_shared8():
     L += ["23:", "s_waitcnt lgkmcnt(0)"]
     L.append("1:")
     unroll = 12  # lcm of BAR8, CSLOTS8, SLOTS8 and the two RB / address buffers (12 for BAR8 = 2 and 3)
+    if not RUN:
+        for j in range(unroll):
+            body_s8(L, j)
+            L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f" if j < unroll - 1 else "s_cbranch_scc0 1b"]
+        L += ["3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
+        epilogue(L)
+        return L
+    # column runs: a tile ends after any of the 12 bodies; its epilogue records the position (S_POS) and the
+    # next tile continues with the following body (ring slots, set slots and address buffers are positions
+    # of the unbroken source-row stream).  Labels: 40 + j = body j, 60 + j = tile end after body j.
     for j in range(unroll):
+        if j:
+            L.append(f"{40 + j}:")
         body_s8(L, j)
-        L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f" if j < unroll - 1 else "s_cbranch_scc0 1b"]
-    L += ["3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
-    epilogue(L)
+        L += [f"s_cmp_eq_u32 s{S_CNT}, 0", f"s_cbranch_scc1 {60 + j}f" if j < unroll - 1 else "s_cbranch_scc0 1b"]
+    for j in [unroll - 1] + list(range(unroll - 1)):
+        L += [f"{60 + j}:", f"s_mov_b32 s{S_POS}, {j}", "s_branch 7f"]
+    L.append("7:")
+    # the run's last tile: the DMA stream's last (re-)reads must land before the workgroup ends (LDS); no other
+    # vmcnt wait follows its stores
+    L += [f"s_cmp_eq_u32 s{S_TL}, 1", "s_cbranch_scc0 26f", "s_waitcnt vmcnt(0)", "26:"]
+    L.append(f"s_mov_b64 s[{S_DST}:{S_DST + 1}], s[{S_DST0}:{S_DST0 + 1}]")
+    epilogue(L)  # the tile's rows (its own rows: S_ROWS), then fresh accumulators
+    L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
+    L += [f"s_sub_u32 s{S_TL}, s{S_TL}, 1",
+          f"s_cmp_eq_u32 s{S_TL}, 0",
+          "s_cbranch_scc1 3f",
+          f"s_add_u32 s{S_DST0}, s{S_DST0}, 4096",
+          f"s_addc_u32 s{S_DST0 + 1}, s{S_DST0 + 1}, 0",
+          f"s_mov_b32 s{S_CNT}, s{S_NIN}"]
+    for j in range(unroll):  # continue with body j + 1
+        nb = "1b" if j == unroll - 1 else f"{40 + j + 1}b"
+        L += [f"s_cmp_eq_u32 s{S_POS}, {j}", f"s_cbranch_scc1 {nb}"]
+    L += ["3:", "s_waitcnt lgkmcnt(0)"]
     return L
 
 
@@ -677,6 +757,8 @@ def epilogue(L):
             for half in range(2):
                 q = 2 * g + half
                 off = f" offset:{q * 1024}" if q else ""
+                if RUN and "rnostore" in DIAG:  # timing only: the column-run program without its tile stores
+                    continue
                 L.append(f"global_store_dwordx4 %[off], v[{V_X + 4 * half}:{V_X + 4 * half + 3}], "
                          f"s[{S_DST}:{S_DST + 1}]{off}")
         L += [f"s_add_u32 s{S_DST}, s{S_DST}, s{S_OUTROW}", f"s_addc_u32 s{S_DST + 1}, s{S_DST + 1}, 0"]
@@ -771,6 +853,11 @@ def main():
         STREAM_J_BYTES = WG_ROWS * 8
         body_txt = "\\n\\t".join(program_shared(cons=True))
         f.write(f'#define RLNC_BSJ_ASM_W8S "{body_txt}"\n')
+        global RUN
+        RUN = True
+        body_txt = "\\n\\t".join(program_shared(cons=True))
+        RUN = False
+        f.write(f'#define RLNC_BSJ_ASM_W8R "{body_txt}"\n')
         f.write(f"#define RLNC_BSJ_SLOTS8 {SLOTS8}\n")
         if SOFFS is not None:  # block offsets of the shared programs' packed table (bsj_offset_kernel<true>)
             f.write("#define RLNC_BSJ_SOFFSETS {" + ", ".join(str(x) for x in SOFFS) + "}\n")

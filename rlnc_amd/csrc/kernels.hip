@@ -946,16 +946,29 @@ __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, in
 // SHARE (W = 4 only): wave w builds one of the four combination sets of each source row and the sets are
 // exchanged through LDS (RLNC_BSJ_ASM_W4S) instead of every wave building all four
 // probe != nullptr (SHARE only): store the block table's address there and return (launch_bsj, once per device)
-template <int W, bool SHARE = false>
+// RUN (W = 8 only, variant 9): the workgroup walks `run` consecutive column blocks of one (object, row tile) --
+// the column-run program (RLNC_BSJ_ASM_W8R) carries the source-row stream across the tile boundaries, so only the
+// first tile pays the prologue (first DMAs, first sets); the grid is objects x row tiles x runs
+template <int W, bool SHARE = false, bool RUN = false>
 __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const void *stream, int row_tiles,
-                                                               int col_blocks, uint64_t *probe) {
+                                                               int col_blocks, uint64_t *probe, int run = 1) {
     static_assert(!SHARE || W == 4 || W == 8, "the shared-set programs are generated for 4 and 8 waves");
+    static_assert(!RUN || (W == 8 && SHARE), "the column-run program is generated for the 8-wave shared program");
     constexpr int kTileRows = kBsjWaveRows * W;
     // W = 8: one workgroup per CU, so a deeper ring and 2 BAR8 set slots (the builders run BAR8 rows ahead)
     __shared__ __attribute__((aligned(16))) uint8_t ring[(W == 8 ? RLNC_BSJ_SLOTS8 : RLNC_BSJ_SLOTS) * kBsjColBlock];
     __shared__ __attribute__((aligned(16))) uint8_t cset[SHARE ? (W == 8 ? RLNC_BSJ_CSET_BYTES8 : RLNC_BSJ_CSET_BYTES) : 16];
     int rt, cb, obj;
-    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    uint32_t tiles = 1;
+    if constexpr (RUN) {
+        const int runs = (col_blocks + run - 1) / run;
+        int r;
+        decode_block(p.n_obj * row_tiles * runs, row_tiles, runs, rt, r, obj);
+        cb = r * run;
+        tiles = uint32_t(__builtin_amdgcn_readfirstlane(min(run, col_blocks - cb)));
+    } else {
+        decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    }
     const int row0 = rt * kTileRows;
     const int rows = min(kTileRows, p.n_out - row0);
     if (p.hdr != nullptr && cb == 0) {  // coded-piece header (encoder.rs:246-248), 64·W threads
@@ -998,13 +1011,14 @@ __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, c
       [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw), [off] "v"(off), \
       [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr), [ldsc] "v"(ldsc), [ldscw] "v"(ldscw), [ldsrg] "v"(ldsrg),           \
       [half] "s"(half), [probe] "s"(probe), [cons] "s"(cons), [ldsc2] "v"(ldsc + 65536u),                        \
-      [ldscw2] "v"(ldscw + 65536u)                                                                                \
+      [ldscw2] "v"(ldscw + 65536u), [tiles] "s"(tiles)                                                            \
     : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S
     if constexpr (W == 1) asm volatile(RLNC_BSJ_ASM_W1 : RLNC_BSJ_OPERANDS);
     if constexpr (W == 2) asm volatile(RLNC_BSJ_ASM_W2 : RLNC_BSJ_OPERANDS);
     if constexpr (W == 4 && !SHARE) asm volatile(RLNC_BSJ_ASM_W4 : RLNC_BSJ_OPERANDS);
     if constexpr (W == 4 && SHARE) asm volatile(RLNC_BSJ_ASM_W4S : RLNC_BSJ_OPERANDS);
-    if constexpr (W == 8) asm volatile(RLNC_BSJ_ASM_W8S : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 8 && !RUN) asm volatile(RLNC_BSJ_ASM_W8S : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 8 && RUN) asm volatile(RLNC_BSJ_ASM_W8R : RLNC_BSJ_OPERANDS);
 #undef RLNC_BSJ_OPERANDS
 #pragma clang diagnostic pop
 }
@@ -1061,8 +1075,30 @@ static hipError_t bsj_shared_base(hipStream_t s, void *scratch, uint64_t &base) 
     return hipSuccess;
 }
 
+// Column blocks per workgroup of the column-run program: enough runs for >= 4 workgroups per CU, at most 8
+// blocks each (RLNC_BSJ_RUN = n forces n; A/B knob, read once)
+static int bsj_run_length(int64_t tiles, int col_blocks, int requested) {
+    static const int forced = [] {
+        const char *e = getenv("RLNC_BSJ_RUN");
+        return e ? atoi(e) : 0;
+    }();
+    static std::mutex mu;
+    static int cus[64] = {};
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        std::lock_guard<std::mutex> lock(mu);
+        if (cus[dev] == 0 && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus[dev] = 256;
+        n = cus[dev] > 0 ? cus[dev] : 256;
+    }
+    int r = requested > 0 ? requested
+            : forced > 0  ? forced
+                          : int(std::min<int64_t>(8, std::max<int64_t>(1, tiles / (int64_t(n) * 4))));
+    return std::max(1, std::min(r, col_blocks));
+}
+
 hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full,
-                      bool share, bool wide) {
+                      bool share, bool wide, bool run) {
     full = (p.width / kBsjColBlock) * kBsjColBlock;
     if (scratch == nullptr || scratch_bytes < bsj_scratch_bytes(p, share && wide)) return hipErrorInvalidValue;
     int W = bsj_waves(p.n_out, share && wide);
@@ -1100,7 +1136,12 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
     else if (W == 2)
         hipLaunchKernelGGL(gf_matmul_bsj_kernel<2>, dim3(unsigned(total)), dim3(128), 0, s, q, stream, row_tiles,
                            col_blocks, nullptr);
-    else if (W == 8)
+    else if (W == 8 && run) {
+        const int rl = bsj_run_length(total, col_blocks, p.col_run);
+        const int64_t units = int64_t(p.n_obj) * row_tiles * ((col_blocks + rl - 1) / rl);
+        hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true, true>), dim3(unsigned(units)), dim3(512), 0, s, q, stream,
+                           row_tiles, col_blocks, nullptr, rl);
+    } else if (W == 8)
         hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true>), dim3(unsigned(total)), dim3(512), 0, s, q, stream,
                            row_tiles, col_blocks, nullptr);
     else if (share)
@@ -1268,11 +1309,13 @@ static bool matmul_aligned(const MatmulParams &p) {
 
 size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v) {
     if ((v != MatmulVariant::BitSliced && v != MatmulVariant::BitSlicedJump && v != MatmulVariant::BitSlicedJumpShared &&
-         v != MatmulVariant::BitSlicedJumpShared8) ||
+         v != MatmulVariant::BitSlicedJumpShared8 && v != MatmulVariant::BitSlicedJumpRun) ||
         p.n_out <= 0 || p.n_in <= 0 || p.n_obj <= 0)
         return 0;
     if (v == MatmulVariant::BitSliced) return bs_eligible(p, matmul_aligned(p)) ? bs_scratch_bytes(p) : 0;
-    return bsj_eligible(p, matmul_aligned(p)) ? bsj_scratch_bytes(p, v == MatmulVariant::BitSlicedJumpShared8) : 0;
+    return bsj_eligible(p, matmul_aligned(p))
+               ? bsj_scratch_bytes(p, v == MatmulVariant::BitSlicedJumpShared8 || v == MatmulVariant::BitSlicedJumpRun)
+               : 0;
 }
 
 hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, void *scratch, size_t scratch_bytes) {
@@ -1280,7 +1323,7 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
     const bool aligned = matmul_aligned(p);
     if (p.n_in <= 0) return hipErrorInvalidValue;
     const bool jump = v == MatmulVariant::BitSlicedJump || v == MatmulVariant::BitSlicedJumpShared ||
-                      v == MatmulVariant::BitSlicedJumpShared8;
+                      v == MatmulVariant::BitSlicedJumpShared8 || v == MatmulVariant::BitSlicedJumpRun;
     if (jump && aligned && p.n_out <= 3 && p.width >= kColBlock) {
         // one to three coded pieces per source pass: HBM-bound, streamed with deep prefetch
         const int64_t full = (p.width / kColBlock) * kColBlock;
@@ -1295,12 +1338,13 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
         return launch_matmul(t, s, MatmulVariant::Perm);
     }
     if (v == MatmulVariant::BitSliced || jump) {
-        const bool share = v == MatmulVariant::BitSlicedJumpShared || v == MatmulVariant::BitSlicedJumpShared8;
-        const bool wide = v == MatmulVariant::BitSlicedJumpShared8;
+        const bool run = v == MatmulVariant::BitSlicedJumpRun;
+        const bool share = v == MatmulVariant::BitSlicedJumpShared || v == MatmulVariant::BitSlicedJumpShared8 || run;
+        const bool wide = v == MatmulVariant::BitSlicedJumpShared8 || run;
         v = MatmulVariant::Perm;  // whatever the bit-sliced kernels do not cover
         if (jump ? bsj_eligible(p, aligned) : bs_eligible(p, aligned)) {
             int64_t full = 0;
-            hipError_t e = jump ? launch_bsj(p, s, scratch, scratch_bytes, full, share, wide)
+            hipError_t e = jump ? launch_bsj(p, s, scratch, scratch_bytes, full, share, wide, run)
                                 : launch_bs(p, s, scratch, scratch_bytes, full);
             if (e != hipSuccess || full == p.width) return e;
             MatmulParams t = p;

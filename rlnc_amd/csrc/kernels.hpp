@@ -26,6 +26,7 @@ struct MatmulParams {
     int n_out, n_in;
     int64_t width;
     int n_obj;
+    int col_run = 0;  // column blocks per workgroup of the column-run program (variant 9): 0 = chosen per launch
 };
 
 enum class MatmulVariant : int {
@@ -37,8 +38,10 @@ enum class MatmulVariant : int {
     BitSliced = 5,
     BitSlicedJump = 6,
     BitSlicedJumpShared = 7,  // 6 with each row's combination sets built once per workgroup (4-wave tiles)
-    BitSlicedJumpShared8 = 8  // 7 with 64-row tiles of 8 waves (n_out > 32): waves 4-7 only read the sets and call,
-                              // the builders run three rows ahead, one barrier per three rows (the default)
+    BitSlicedJumpShared8 = 8,  // 7 with 64-row tiles of 8 waves (n_out > 32): waves 4-7 only read the sets and call,
+                               // the builders run three rows ahead, one barrier per three rows
+    BitSlicedJumpRun = 9       // 8 with column runs: a workgroup walks up to 8 column blocks of one (object, row
+                               // tile), the source-row stream unbroken across them (one prologue per run)
 };
 
 // Device scratch the BitSliced variant needs for its coefficient-index stream (0 for the others, and for

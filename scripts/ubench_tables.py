@@ -36,55 +36,100 @@ def block_indices(c):
     return lo, hi
 
 
+# Register maps.  "std": the product kernel's (accumulators v0-v127 with row slot i at 16 i, combinations
+# v128-v191); "bank": every XOR3's three sources in three different VGPR banks (bank = vN mod 4) -- accumulators
+# in banks 2 and 3 (row slot i at 32 i, M0 steps by 32), the low-half combinations in bank 0, the high-half ones
+# in bank 1 (v0-v125).
+MAP = "std"
+
+
 def G(g, h, v):
+    if MAP == "bank":
+        return 4 * (16 * g + v) + h
     return 128 + g * 32 + h * 16 + v
 
 
-def block_body(c, slot, relative, reps=1):
+def ACC(i, g, p):
+    if MAP == "bank":
+        return 32 * i + 4 * (4 * g + p // 2) + 2 + p % 2
+    return 16 * i + 8 * g + p
+
+
+def SLOT_STEP():
+    return 32 if MAP == "bank" else 16
+
+
+def REGS():
+    return sorted({ACC(i, g, p) for i in range(8) for g in range(2) for p in range(8)} |
+                  {G(g, h, v) for g in range(2) for h in range(2) for v in range(16)})
+
+
+def block_body(c, slot, relative, reps=1, pack=False):
     lo, hi = block_indices(c)
     L = []
     for _ in range(reps):
+        v3, v2 = [], []
         for g in range(2):
             for o in range(8):
-                a = (0 if relative else slot * 16) + g * 8 + o
+                a = ACC(0 if relative else slot, g, o)
+                if pack:  # the product kernel's packed form: accumulator as SRC0, VOP2 XOR for a one-half product
+                    if lo[o] and hi[o]:
+                        v3.append(f"v_bitop3_b32 v{a}, v{a}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])} bitop3:0x96")
+                    elif lo[o] or hi[o]:
+                        v2.append(f"v_xor_b32 v{a}, v{a}, v{G(g, 0, lo[o]) if lo[o] else G(g, 1, hi[o])}")
+                    continue
                 x = f"v{G(g, 0, lo[o])}" if lo[o] else "0"
                 y = f"v{G(g, 1, hi[o])}" if hi[o] else "0"
                 L.append(f"v_bitop3_b32 v{a}, {x}, {y}, v{a} bitop3:0x96")
+        L += v3 + v2
     return L
 
 
-def blocks(slot, relative, reps=1, stride=None, empty=False):
+def body_bytes(c, reps, pack):
+    if not pack:
+        return 16 * reps * 8
+    return sum(8 if x.startswith("v_bitop3") else 4 for x in block_body(c, 0, True, reps, True))
+
+
+def blocks(slot, relative, reps=1, stride=None, empty=False, pack=False):
     """256 blocks; each 16 * reps XOR3s (none if empty) + s_setpc, padded with s_nop to `stride` bytes."""
     L = []
-    size = (0 if empty else 16 * reps * 8) + 4
-    stride = stride or size
+    stride = stride or (0 if empty else 16 * reps * 8) + 4
     for c in range(256):
+        size = (0 if empty else body_bytes(c, reps, pack)) + 4
         if not empty:
-            L += block_body(c, slot, relative, reps)
+            L += block_body(c, slot, relative, reps, pack)
         L.append("s_setpc_b64 s[40:41]")
         L += ["s_nop 0"] * ((stride - size) // 4)
     return L
 
 
-MODES = {  # name: (tables, relative, xor3 reps per block, stride, empty, inline)
-    "rel1": (1, True, 1, None, False, False),
-    "abs1": (1, False, 1, None, False, False),
-    "rel1_a256": (1, True, 1, 256, False, False),
-    "empty": (1, False, 1, None, True, False),
-    "rel1_x2": (1, True, 2, None, False, False),
-    "inline_rel": (0, True, 1, None, False, True),
-    "inline_abs": (0, False, 1, None, False, True),
+MODES = {  # name: (tables, relative, xor3 reps per block, stride, empty, inline, map, pack)
+    "rel1": (1, True, 1, None, False, False, "std", False),
+    "abs1": (1, False, 1, None, False, False, "std", False),
+    "rel1_a256": (1, True, 1, 256, False, False, "std", False),
+    "empty": (1, False, 1, None, True, False, "std", False),
+    "rel1_x2": (1, True, 2, None, False, False, "std", False),
+    "inline_rel": (0, True, 1, None, False, True, "std", False),
+    "inline_abs": (0, False, 1, None, False, True, "std", False),
+    # round 2: the packed blocks of the product kernel (stride 136), standard and bank-separated register maps
+    "relp": (1, True, 1, 136, False, False, "std", True),
+    "relp_bank": (1, True, 1, 136, False, False, "bank", True),
+    "inline_relp": (0, True, 1, None, False, True, "std", True),
+    "inline_relp_bank": (0, True, 1, None, False, True, "bank", True),
+    "inline_abs_bank": (0, False, 1, None, False, True, "bank", False),
 }
 
 
 def block_stride(mode):
-    tables, rel, reps, stride, empty, inl = MODES[mode]
+    tables, rel, reps, stride, empty, inl, mp, pack = MODES[mode]
     size = (0 if empty else 16 * reps * 8) + 4
     return stride or size
 
 
 def program(mode):
-    tables, rel, reps, stride, empty, inl = MODES[mode]
+    global MAP
+    tables, rel, reps, stride, empty, inl, MAP, pack = MODES[mode]
     bs = block_stride(mode)
     # the tables sit first and the entry jumps over them with s_setpc (big tables are beyond s_branch's range)
     L = ["s_getpc_b64 s[36:37]", "2:", "s_add_u32 s36, s36, (9f - 2b)", "s_addc_u32 s37, s37, 0",
@@ -92,18 +137,18 @@ def program(mode):
          "s_getpc_b64 s[54:55]", "3:", "s_add_u32 s54, s54, (7f - 3b)", "s_addc_u32 s55, s55, 0",
          "s_setpc_b64 s[54:55]", ".p2align 8", "9:"]
     for t in range(tables):
-        L += blocks(t, rel, reps, stride, empty)
+        L += blocks(t, rel, reps, stride, empty, pack)
     L.append("7:")
     if rel:
-        L.append("s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)")
+        L.append(f"s_set_gpr_idx_on 0, {'gpr_idx(SRC0,DST)' if pack else 'gpr_idx(SRC2,DST)'}")
     L.append("1:")
     L += ["s_load_dwordx8 s[44:51], s[52:53], 0", "s_add_u32 s52, s52, 32", "s_addc_u32 s53, s53, 0",
           "s_waitcnt lgkmcnt(0)"]
     for i in range(8):
         if rel:
-            L.append(f"s_mov_b32 m0, {hex(0xC000 | (16 * i))}")
+            L.append(f"s_mov_b32 m0, {hex((0x9000 if pack else 0xC000) | (SLOT_STEP() * i))}")
         if inl:  # the products of a fixed coefficient per row, no call
-            L += block_body(0x53 + i, i, rel)
+            L += block_body(0x53 + i, i, rel, 1, pack)
             continue
         L += [f"s_add_u32 s38, s36, s{44 + i}", "s_addc_u32 s39, s37, 0"]  # offsets hold c * this stride
         L.append("s_swappc_b64 s[40:41], s[38:39]")
@@ -114,12 +159,16 @@ def program(mode):
 
 
 def gen(path):
-    clob = ", ".join(f'"v{r}"' for r in range(192)) + ", " + ", ".join(f'"s{r}"' for r in range(36, 56))
+    global MAP
     modes = list(MODES)
     src = ['#include <hip/hip_runtime.h>', '#include <cstdio>', '#include <vector>', '#include <cstdint>']
-    movs = "\n".join(f'                 "v_mov_b32 v{r}, v{r % 4}\\n"' for r in range(4, 192))
     for mi, mode in enumerate(modes):
         prog = program(mode)
+        regs = REGS()
+        MAP = "std"
+        regs = sorted(set(regs) | set(range(4)))
+        clob = ", ".join(f'"v{r}"' for r in regs) + ", " + ", ".join(f'"s{r}"' for r in range(36, 56))
+        movs = "\n".join(f'                 "v_mov_b32 v{r}, v{r % 4}\\n"' for r in regs if r >= 4)
         src.append(f'''
 __global__ __launch_bounds__(256) void k_{mode}(unsigned long long *out, int reps, const uint32_t *offs,
                                                  const uint32_t *seed) {{
@@ -137,7 +186,7 @@ __global__ __launch_bounds__(256) void k_{mode}(unsigned long long *out, int rep
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
     uint32_t acc;
-    asm volatile("v_xor_b32 %0, v0, v17\\n v_xor_b32 %0, %0, v127" : "=v"(acc) :: {clob});
+    asm volatile("v_xor_b32 %0, v0, v{regs[17]}\\n v_xor_b32 %0, %0, v{regs[-1]}" : "=v"(acc) :: {clob});
     if (threadIdx.x % 64 == 0) {{
         const int w = blockIdx.x * 4 + threadIdx.x / 64;
         out[4 * w + 0] = t1 - t0;

@@ -68,7 +68,7 @@ SHAPES = [(1, 1, 1, 1), (1, 3, 17, 1), (2, 2, 16, 2), (3, 5, 4095, 1), (4, 32, 4
           (9, 40, 32768, 1), (1, 32, 8192 + 16, 2), (2, 7, 4096, 1), (3, 33, 12288 + 48, 2), (1, 70, 4096 * 5, 1)]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("n_out,n_in,W,nobj", SHAPES)
 def test_matmul(ctx, variant, n_out, n_in, W, nobj):
     from rlnc_amd import batch
@@ -97,7 +97,7 @@ BS_SHAPES = [(4, 1, 16384, 1), (5, 2, 16384 + 16, 2), (8, 32, 32768, 1), (9, 31,
              (3, 5, 16384, 1)]
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [5, 6, 7, 8, 9])
 @pytest.mark.parametrize("n_out,n_in,W,nobj", BS_SHAPES)
 def test_matmul_bitsliced(ctx, variant, n_out, n_in, W, nobj):
     from rlnc_amd import batch
@@ -146,6 +146,37 @@ def test_matmul_eight_wave_tiles(ctx, n_out, n_in, W, nobj):
         assert np.array_equal(got[o], np_matmul(coef[o], inp[o])), o
 
 
+# variant 9: column runs (a workgroup walks `run` column blocks with its source-row stream unbroken); forced run
+# lengths against ragged runs, fewer sources than the DMA depth (the stream crosses several tiles at once), source
+# counts off the 12-row unroll, partial row tiles and the ragged byte tail
+RUN_SHAPES = [(64, 32, 4096 * 5, 2), (33, 1, 4096 * 7 + 17, 1), (70, 2, 4096 * 4, 2), (40, 3, 4096 * 9, 1),
+              (100, 13, 4096 * 6 + 48, 1), (128, 25, 4096 * 3, 2), (64, 12, 4096 * 8, 1), (65, 7, 4096 * 5, 3)]
+
+
+@pytest.mark.parametrize("run", [0, 1, 2, 3, 8])
+@pytest.mark.parametrize("n_out,n_in,W,nobj", RUN_SHAPES)
+def test_matmul_column_runs(ctx, run, n_out, n_in, W, nobj):
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(n_out * 13 + n_in * 7 + W + nobj + run)
+    coef = rng.integers(0, 256, (nobj, n_out, n_in), dtype=np.uint8)
+    coef[:, 0, :] = 1
+    coef[:, -1, :] = 0
+    inp = rng.integers(0, 256, (nobj, n_in, W), dtype=np.uint8)
+    inp[:, 0, :256] = np.arange(256, dtype=np.uint8)
+    out = dev(np.zeros((nobj, n_out, W), np.uint8))
+    ctx.set_kernel_variant(9, 0)
+    ctx.set_column_run(run)
+    try:
+        batch.matmul(dev(coef), dev(inp), out, ctx)
+        got = host(out)
+    finally:
+        ctx.set_kernel_variant(DEFAULT_VARIANT, 0)
+        ctx.set_column_run(0)
+    for o in range(nobj):
+        assert np.array_equal(got[o], np_matmul(coef[o], inp[o])), o
+
+
 def test_matmul_every_coefficient_eight_waves(ctx):
     """All 256 coefficients in a 64-row tile (64 rows x 4 sources), each against every byte value."""
     from rlnc_amd import batch
@@ -184,7 +215,7 @@ def test_matmul_every_coefficient(ctx, variant):
     assert np.array_equal(got[0], np_matmul(coef[0], inp[0]))
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [5, 6, 7, 8, 9])
 @pytest.mark.parametrize("n_out", [12, 40, 70])
 def test_matmul_bitsliced_strided_with_header(ctx, variant, n_out):
     """Padded row strides and the coded-piece header copy, through the raw C ABI descriptor; n_out > 32 reaches
