@@ -578,6 +578,45 @@ def program_shared_body(cons=False):
 SOFFS = None  # byte offsets of the shared programs' packed blocks (--pack)
 
 
+def run_tail(L, unroll, body_fn):
+    """The column-run main loop: `unroll` bodies, a tile ending after any of them (labels: 40 + j = body j,
+    60 + j = tile end after body j); the tile end records the position (S_POS), runs the epilogue into the
+    tile's rows, clears the accumulators and continues with the next body while the run has tiles."""
+    L.append("1:")
+    for j in range(unroll):
+        if j:
+            L.append(f"{40 + j}:")
+        body_fn(L, j)
+        L += [f"s_cmp_eq_u32 s{S_CNT}, 0", f"s_cbranch_scc1 {60 + j}f" if j < unroll - 1 else "s_cbranch_scc0 1b"]
+    for j in [unroll - 1] + list(range(unroll - 1)):
+        L += [f"{60 + j}:", f"s_mov_b32 s{S_POS}, {j}", "s_branch 7f"]
+    L.append("7:")
+    # the run's last tile: the DMA stream's last (re-)reads must land before the workgroup ends (LDS); no other
+    # vmcnt wait follows its stores
+    L += [f"s_cmp_eq_u32 s{S_TL}, 1", "s_cbranch_scc0 26f", "s_waitcnt vmcnt(0)", "26:"]
+    L.append(f"s_mov_b64 s[{S_DST}:{S_DST + 1}], s[{S_DST0}:{S_DST0 + 1}]")
+    epilogue(L)  # the tile's rows (its own rows: S_ROWS), then fresh accumulators
+    L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
+    L += [f"s_sub_u32 s{S_TL}, s{S_TL}, 1",
+          f"s_cmp_eq_u32 s{S_TL}, 0",
+          "s_cbranch_scc1 3f",
+          f"s_add_u32 s{S_DST0}, s{S_DST0}, 4096",
+          f"s_addc_u32 s{S_DST0 + 1}, s{S_DST0 + 1}, 0",
+          f"s_mov_b32 s{S_CNT}, s{S_NIN}"]
+    for j in range(unroll):  # continue with body j + 1
+        nb = "1b" if j == unroll - 1 else f"{40 + j + 1}b"
+        L += [f"s_cmp_eq_u32 s{S_POS}, {j}", f"s_cbranch_scc1 {nb}"]
+    L += ["3:", "s_waitcnt lgkmcnt(0)"]
+
+
+def run_init(L):
+    L += [f"s_mov_b64 s[{S_SRCT}:{S_SRCT + 1}], %[src]",
+          f"s_mov_b64 s[{S_DST0}:{S_DST0 + 1}], %[dst]",
+          f"s_mov_b32 s{S_TL}, %[tiles]",
+          f"s_mov_b32 s{S_DTL}, %[tiles]",
+          f"s_mov_b32 s{S_NIN}, %[n_in]"]
+
+
 # 8-wave program: one workgroup per CU leaves LDS for SLOTS8 ring slots and CSLOTS8 = 2 BAR8 set slots, so the
 # builders run BAR8 rows ahead (staging read of row j + BAR8 + 1, set of row j + BAR8, DMA of row j + DMA8 during
 # row j) and the workgroup meets at a barrier every BAR8-th row instead of every row.  Conditions (vmcnt(1) at
@@ -658,11 +697,7 @@ def body_s8(L, j):
 def program_shared8():
     L = []
     if RUN:
-        L += [f"s_mov_b64 s[{S_SRCT}:{S_SRCT + 1}], %[src]",
-              f"s_mov_b64 s[{S_DST0}:{S_DST0 + 1}], %[dst]",
-              f"s_mov_b32 s{S_TL}, %[tiles]",
-              f"s_mov_b32 s{S_DTL}, %[tiles]",
-              f"s_mov_b32 s{S_NIN}, %[n_in]"]
+        run_init(L)
     L += [
         f"s_mov_b64 s[{S_SRC}:{S_SRC + 1}], %[src]",
         f"s_mov_b64 s[{S_IDX}:{S_IDX + 1}], %[idx]",
@@ -709,42 +744,18 @@ def program_shared8():
                 L.append(f"ds_read_b128 v[{x}:{x + 3}], %[ldsrg] offset:{(r + 2) * 4096 + hh * 1024}")
         L.append("s_waitcnt lgkmcnt(0)")  # the set writes have read OWN; the staged row is in
     L += ["23:", "s_waitcnt lgkmcnt(0)"]
-    L.append("1:")
     unroll = 12  # lcm of BAR8, CSLOTS8, SLOTS8 and the two RB / address buffers (12 for BAR8 = 2 and 3)
     if not RUN:
+        L.append("1:")
         for j in range(unroll):
             body_s8(L, j)
             L += [f"s_cmp_eq_u32 s{S_CNT}, 0", "s_cbranch_scc1 3f" if j < unroll - 1 else "s_cbranch_scc0 1b"]
         L += ["3:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
         epilogue(L)
         return L
-    # column runs: a tile ends after any of the 12 bodies; its epilogue records the position (S_POS) and the
-    # next tile continues with the following body (ring slots, set slots and address buffers are positions
-    # of the unbroken source-row stream).  Labels: 40 + j = body j, 60 + j = tile end after body j.
-    for j in range(unroll):
-        if j:
-            L.append(f"{40 + j}:")
-        body_s8(L, j)
-        L += [f"s_cmp_eq_u32 s{S_CNT}, 0", f"s_cbranch_scc1 {60 + j}f" if j < unroll - 1 else "s_cbranch_scc0 1b"]
-    for j in [unroll - 1] + list(range(unroll - 1)):
-        L += [f"{60 + j}:", f"s_mov_b32 s{S_POS}, {j}", "s_branch 7f"]
-    L.append("7:")
-    # the run's last tile: the DMA stream's last (re-)reads must land before the workgroup ends (LDS); no other
-    # vmcnt wait follows its stores
-    L += [f"s_cmp_eq_u32 s{S_TL}, 1", "s_cbranch_scc0 26f", "s_waitcnt vmcnt(0)", "26:"]
-    L.append(f"s_mov_b64 s[{S_DST}:{S_DST + 1}], s[{S_DST0}:{S_DST0 + 1}]")
-    epilogue(L)  # the tile's rows (its own rows: S_ROWS), then fresh accumulators
-    L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
-    L += [f"s_sub_u32 s{S_TL}, s{S_TL}, 1",
-          f"s_cmp_eq_u32 s{S_TL}, 0",
-          "s_cbranch_scc1 3f",
-          f"s_add_u32 s{S_DST0}, s{S_DST0}, 4096",
-          f"s_addc_u32 s{S_DST0 + 1}, s{S_DST0 + 1}, 0",
-          f"s_mov_b32 s{S_CNT}, s{S_NIN}"]
-    for j in range(unroll):  # continue with body j + 1
-        nb = "1b" if j == unroll - 1 else f"{40 + j + 1}b"
-        L += [f"s_cmp_eq_u32 s{S_POS}, {j}", f"s_cbranch_scc1 {nb}"]
-    L += ["3:", "s_waitcnt lgkmcnt(0)"]
+    # column runs (run_tail): ring slots, set slots and address buffers are positions of the unbroken
+    # source-row stream, so the next tile continues with the body after the one its predecessor ended in
+    run_tail(L, unroll, body_s8)
     return L
 
 

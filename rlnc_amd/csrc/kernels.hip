@@ -953,6 +953,8 @@ template <int W, bool SHARE = false, bool RUN = false>
 __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const void *stream, int row_tiles,
                                                                int col_blocks, uint64_t *probe, int run = 1) {
     static_assert(!SHARE || W == 4 || W == 8, "the shared-set programs are generated for 4 and 8 waves");
+    // (a 4-wave run program measured no gain: two workgroups per CU already hide the 32-row tile's prologue,
+    // profiles/r02_run_ab.txt)
     static_assert(!RUN || (W == 8 && SHARE), "the column-run program is generated for the 8-wave shared program");
     constexpr int kTileRows = kBsjWaveRows * W;
     // W = 8: one workgroup per CU, so a deeper ring and 2 BAR8 set slots (the builders run BAR8 rows ahead)

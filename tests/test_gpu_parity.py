@@ -149,8 +149,11 @@ def test_matmul_eight_wave_tiles(ctx, n_out, n_in, W, nobj):
 # variant 9: column runs (a workgroup walks `run` column blocks with its source-row stream unbroken); forced run
 # lengths against ragged runs, fewer sources than the DMA depth (the stream crosses several tiles at once), source
 # counts off the 12-row unroll, partial row tiles and the ragged byte tail
+# (17-32 output rows: the 4-wave run program)
 RUN_SHAPES = [(64, 32, 4096 * 5, 2), (33, 1, 4096 * 7 + 17, 1), (70, 2, 4096 * 4, 2), (40, 3, 4096 * 9, 1),
-              (100, 13, 4096 * 6 + 48, 1), (128, 25, 4096 * 3, 2), (64, 12, 4096 * 8, 1), (65, 7, 4096 * 5, 3)]
+              (100, 13, 4096 * 6 + 48, 1), (128, 25, 4096 * 3, 2), (64, 12, 4096 * 8, 1), (65, 7, 4096 * 5, 3),
+              (32, 32, 4096 * 5, 2), (17, 1, 4096 * 7 + 17, 1), (24, 2, 4096 * 4, 2), (20, 5, 4096 * 9, 1),
+              (32, 13, 4096 * 6 + 48, 1), (30, 7, 4096 * 3, 3)]
 
 
 @pytest.mark.parametrize("run", [0, 1, 2, 3, 8])
