@@ -951,7 +951,8 @@ __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, in
 // first tile pays the prologue (first DMAs, first sets); the grid is objects x row tiles x runs
 template <int W, bool SHARE = false, bool RUN = false>
 __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const void *stream, int row_tiles,
-                                                               int col_blocks, uint64_t *probe, int run = 1) {
+                                                               int col_blocks, uint64_t *probe, int run = 1,
+                                                               int guided_nl = -1) {
     static_assert(!SHARE || W == 4 || W == 8, "the shared-set programs are generated for 4 and 8 waves");
     // (a 4-wave run program measured no gain: two workgroups per CU already hide the 32-row tile's prologue,
     // profiles/r02_run_ab.txt)
@@ -965,9 +966,31 @@ __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, c
     if constexpr (RUN) {
         const int runs = (col_blocks + run - 1) / run;
         int r;
-        decode_block(p.n_obj * row_tiles * runs, row_tiles, runs, rt, r, obj);
-        cb = r * run;
-        tiles = uint32_t(__builtin_amdgcn_readfirstlane(min(run, col_blocks - cb)));
+        if (guided_nl < 0) {
+            decode_block(p.n_obj * row_tiles * runs, row_tiles, runs, rt, r, obj);
+            cb = r * run;
+            tiles = uint32_t(__builtin_amdgcn_readfirstlane(min(run, col_blocks - cb)));
+        } else {
+            // guided runs (launch_bsj checked: run | col_blocks, 8 | the run units): XCD x = b & 7 owns run units
+            // [x·per, (x+1)·per) (rt fastest, as decode_block), its first guided_nl dispatched workgroups walk one
+            // unit each, the later ones one column block of the remaining units -- short workgroups last
+            const int per = (p.n_obj * row_tiles * runs) >> 3;
+            const int b = blockIdx.x, x = b & 7, i = b >> 3;
+            int u, c = 0;
+            if (i < guided_nl) {
+                u = x * per + i;
+                tiles = uint32_t(run);
+            } else {
+                const int j = i - guided_nl;
+                u = x * per + guided_nl + j / run;
+                c = j % run;
+            }
+            rt = u % row_tiles;
+            const int rest = u / row_tiles;
+            r = rest % runs;
+            obj = rest / runs;
+            cb = r * run + c;
+        }
     } else {
         decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
     }
@@ -1099,6 +1122,16 @@ static int bsj_run_length(int64_t tiles, int col_blocks, int requested) {
     return std::max(1, std::min(r, col_blocks));
 }
 
+// Guided column runs (variant 9): percentage of each XCD's run units walked as whole runs, the rest as single
+// column blocks dispatched last (RLNC_BSJ_GUIDED; -1 = plain runs).  A/B knob, read once.
+static int bsj_guided_pct() {
+    static const int pct = [] {
+        const char *e = getenv("RLNC_BSJ_GUIDED");
+        return e ? std::max(-1, std::min(100, atoi(e))) : -1;
+    }();
+    return pct;
+}
+
 hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full,
                       bool share, bool wide, bool run) {
     full = (p.width / kBsjColBlock) * kBsjColBlock;
@@ -1141,8 +1174,18 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
     else if (W == 8 && run) {
         const int rl = bsj_run_length(total, col_blocks, p.col_run);
         const int64_t units = int64_t(p.n_obj) * row_tiles * ((col_blocks + rl - 1) / rl);
-        hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true, true>), dim3(unsigned(units)), dim3(512), 0, s, q, stream,
-                           row_tiles, col_blocks, nullptr, rl);
+        const int pct = bsj_guided_pct();
+        if (pct >= 0 && rl > 1 && col_blocks % rl == 0 && units % 8 == 0) {
+            // guided: per XCD, pct % of the run units as whole runs (dispatched first), the rest one block each
+            const int64_t per = units / 8;
+            const int64_t nl = per * pct / 100;
+            const int64_t wgs = 8 * (nl + (per - nl) * rl);
+            hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true, true>), dim3(unsigned(wgs)), dim3(512), 0, s, q, stream,
+                               row_tiles, col_blocks, nullptr, rl, int(nl));
+        } else {
+            hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true, true>), dim3(unsigned(units)), dim3(512), 0, s, q,
+                               stream, row_tiles, col_blocks, nullptr, rl, -1);
+        }
     } else if (W == 8)
         hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true>), dim3(unsigned(total)), dim3(512), 0, s, q, stream,
                            row_tiles, col_blocks, nullptr);

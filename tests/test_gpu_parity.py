@@ -153,7 +153,9 @@ def test_matmul_eight_wave_tiles(ctx, n_out, n_in, W, nobj):
 RUN_SHAPES = [(64, 32, 4096 * 5, 2), (33, 1, 4096 * 7 + 17, 1), (70, 2, 4096 * 4, 2), (40, 3, 4096 * 9, 1),
               (100, 13, 4096 * 6 + 48, 1), (128, 25, 4096 * 3, 2), (64, 12, 4096 * 8, 1), (65, 7, 4096 * 5, 3),
               (32, 32, 4096 * 5, 2), (17, 1, 4096 * 7 + 17, 1), (24, 2, 4096 * 4, 2), (20, 5, 4096 * 9, 1),
-              (32, 13, 4096 * 6 + 48, 1), (30, 7, 4096 * 3, 3)]
+              (32, 13, 4096 * 6 + 48, 1), (30, 7, 4096 * 3, 3),
+              # guided runs need 8 | run units and run | column blocks (whole runs first, single blocks last)
+              (64, 32, 4096 * 8, 8), (70, 5, 4096 * 4, 4), (128, 25, 4096 * 6 + 48, 4), (64, 3, 4096 * 16, 4)]
 
 
 @pytest.mark.parametrize("run", [0, 1, 2, 3, 8])
