@@ -719,3 +719,44 @@ def test_config5_batch_objects_k128_64KiB(ctx, orc):
     for o in range(nobj):
         if (pst[o] == 0).sum() == k:  # full rank: decode must return the source rows
             assert np.array_equal(got[o], src[o])
+
+
+# ------------------------------------------------------------------------------------------------
+# large piece counts: k at and past 255/256 (the reference takes any piece_count, encoder.rs:85-106), full encode
+# through the batch API, decode with the default path (k + m > 256: the round-1 device kernel, or the host
+# elimination once [coeffs | E] outgrows LDS) and with the host elimination (path 1)
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("k,extra,L", [(255, 3, 4096 + 16), (256, 4, 4096), (300, 8, 8192 + 48)])
+@pytest.mark.parametrize("path", [0, 1])
+def test_large_piece_counts(ctx, orc, k, extra, L, path):
+    import torch
+
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(k * 31 + extra + path)
+    nobj, n = 2, k + extra
+    src = rng.integers(0, 256, (nobj, k, L), dtype=np.uint8)
+    coeffs = rng.integers(0, 256, (nobj, n, k), dtype=np.uint8)
+    coeffs[:, k, :] = coeffs[:, 0, :]  # a repeated coefficient vector: PieceNotUseful mid-sequence
+    pieces = torch.zeros((nobj, n, k + L), dtype=torch.uint8, device="cuda:0")
+    batch.encode_batch(dev(src), dev(coeffs), pieces, ctx)
+    hp = host(pieces)
+    for o in range(nobj):
+        assert np.array_equal(hp[o], orc.encode(src[o], coeffs[o])), o
+    decoded = dev(np.zeros((nobj, k, L), np.uint8))
+    ctx.set_decode_path(path)
+    try:
+        pst, ost, dl = batch.decode_batch(pieces, k, decoded, ctx)
+    finally:
+        ctx.set_decode_path(0)
+    got = host(decoded)
+    for o in range(nobj):
+        od = OracleDecoder(L, k)
+        want = [S[od.decode(p)] for p in hp[o]]
+        assert [S[x] for x in pst[o]] == want, o
+        pay = od.padded_payload()
+        assert np.array_equal(got[o, : pay.shape[0]], pay), o
+        st, _ = od.get_decoded_data()
+        assert S[ost[o]] == S[st], o
+        if want.count("Ok") == k:
+            assert np.array_equal(got[o], src[o]), o
