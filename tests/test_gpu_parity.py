@@ -760,3 +760,23 @@ def test_large_piece_counts(ctx, orc, k, extra, L, path):
         assert S[ost[o]] == S[st], o
         if want.count("Ok") == k:
             assert np.array_equal(got[o], src[o]), o
+
+
+@pytest.mark.parametrize("k,n,count", [(256, 260, 70), (300, 300, 33)])
+def test_large_piece_count_recode(ctx, orc, k, n, count):
+    """Recode of n coded pieces with k ≥ 256 (recoder.rs:122-153: the coefficient fold and the data combination
+    as one linear map over the full pieces): every recoded piece against the oracle's recode."""
+    import torch
+
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(k + n + count)
+    L = 4096 + 32
+    src = rng.integers(0, 256, (k, L), dtype=np.uint8)
+    pieces = orc.encode(src, rng.integers(0, 256, (n, k), dtype=np.uint8))
+    r = rng.integers(0, 256, (1, count, n), dtype=np.uint8)
+    out = torch.zeros((1, count, k + L), dtype=torch.uint8, device="cuda:0")
+    batch.recode_batch(dev(pieces[None]), dev(r), out, k, ctx)
+    got = host(out)[0]
+    for c in range(count):
+        assert np.array_equal(got[c], orc.recode(pieces, k + L, k, r[0, c])), c
