@@ -817,6 +817,22 @@ def program():
     return L
 
 
+# cache-policy modifiers of the source DMA loads and the tile stores (--load-hint / --store-hint, A/B only; the
+# default program carries none)
+HINTS = {"load": "", "store": ""}
+
+
+def hinted(lines):
+    out = []
+    for ln in lines:
+        if HINTS["load"] and ln.startswith("global_load_lds_dwordx4"):
+            ln += " " + HINTS["load"]
+        if HINTS["store"] and ln.startswith("global_store_dwordx4"):
+            ln += " " + HINTS["store"]
+        out.append(ln)
+    return out
+
+
 def main():
     global BLOCK_BYTES, ALIGN, WAVES, WG_ROWS, STREAM_J_BYTES
     ap = argparse.ArgumentParser()
@@ -829,7 +845,10 @@ def main():
     ap.add_argument("--no-m0step", action="store_true", help="shared programs: M0 moved as a literal per call")
     ap.add_argument("--no-pack", action="store_true", help="shared programs: fixed-stride XOR3-only blocks")
     ap.add_argument("--prio", default="", help="K,L: shared program's calls K.. of each row at s_setprio L")
+    ap.add_argument("--load-hint", default="", help="cache-policy modifiers of the DMA loads, e.g. 'nt' (A/B)")
+    ap.add_argument("--store-hint", default="", help="cache-policy modifiers of the tile stores, e.g. 'nt' (A/B)")
     args = ap.parse_args()
+    HINTS["load"], HINTS["store"] = args.load_hint, args.store_hint
     global PRIO_AT
     if args.prio:
         PRIO_AT = None if args.prio == "off" else tuple(int(x) for x in args.prio.split(","))
@@ -854,19 +873,19 @@ def main():
         for w in (1, 2, 4):
             WAVES, WG_ROWS = w, NT * w
             STREAM_J_BYTES = WG_ROWS * 4
-            body_txt = "\\n\\t".join(program())
+            body_txt = "\\n\\t".join(hinted(program()))
             f.write(f'#define RLNC_BSJ_ASM_W{w} "{body_txt}"\n')
         WAVES, WG_ROWS = 4, NT * 4
         STREAM_J_BYTES = WG_ROWS * 8  # 64-bit block addresses
-        body_txt = "\\n\\t".join(program_shared())
+        body_txt = "\\n\\t".join(hinted(program_shared()))
         f.write(f'#define RLNC_BSJ_ASM_W4S "{body_txt}"\n')
         WAVES, WG_ROWS = 8, NT * 8
         STREAM_J_BYTES = WG_ROWS * 8
-        body_txt = "\\n\\t".join(program_shared(cons=True))
+        body_txt = "\\n\\t".join(hinted(program_shared(cons=True)))
         f.write(f'#define RLNC_BSJ_ASM_W8S "{body_txt}"\n')
         global RUN
         RUN = True
-        body_txt = "\\n\\t".join(program_shared(cons=True))
+        body_txt = "\\n\\t".join(hinted(program_shared(cons=True)))
         RUN = False
         f.write(f'#define RLNC_BSJ_ASM_W8R "{body_txt}"\n')
         f.write(f"#define RLNC_BSJ_SLOTS8 {SLOTS8}\n")
