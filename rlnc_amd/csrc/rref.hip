@@ -1365,8 +1365,14 @@ static size_t rref_lds_bytes_staged(int k, int m) {
 
 hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     if (p.n_obj <= 0) return hipSuccess;
+    // many small objects (k <= 16, >= 2048 of them: 8 per CU and more): the one-wave register kernel (path 4's)
+    // beats the 4-wave blocked run, whose per-object parallelism the full grid no longer needs -- 4,096 x k = 16:
+    // 0.093 vs 0.125 ms, k = 8: 0.051 vs 0.067, k = 16 sparse + dependent: 0.195 vs 0.295; at 512 objects the
+    // blocked run stays faster (0.035 vs 0.049) (profiles/r02_elim_small_k.jsonl)
+    const bool small_many = p.lds_only == 0 && p.k <= 16 && p.n_obj >= 2048 && rref_row_dwords(p.k, p.m) <= 16 &&
+                            rref_lds_bytes_staged(p.k, p.m) <= kRrefMaxLds;
     // the blocked clean run (4 waves per object, the default) when the row fits one wave (k + m <= 256)
-    if ((p.lds_only == 0 || p.lds_only == 3) && rref_row_dwords(p.k, p.m) <= 64 &&
+    if (!small_many && (p.lds_only == 0 || p.lds_only == 3) && rref_row_dwords(p.k, p.m) <= 64 &&
         rref_block_lds_bytes(p.k, p.m) <= kRrefMaxLds) {
         // A/B knob (read once): RLNC_BLK = 8 or 16 pieces per block (NW = 4 waves)
         // A/B knob (read once): RLNC_BLK = 8 or 16 pieces per block (profiles/r02_elim_ab.txt)
@@ -1406,7 +1412,7 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     auto kern = &gf_rref_batch_kernel<0, 1, 1>;
     int threads = 64;
     if (p.lds_only != 1 && hdr_lds) {  // the register paths read the staged headers
-        const bool mw = p.lds_only == 0 || p.lds_only == 4;
+        const bool mw = (p.lds_only == 0 && !small_many) || p.lds_only == 4;
         if (D <= 16 && p.k <= 32) {
             kern = mw ? &gf_rref_batch_kernel<4, 8, 4, 4, 2> : &gf_rref_batch_kernel<4, 8, 1>;
         } else if (D <= 32 && p.k <= 64) {

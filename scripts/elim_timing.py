@@ -25,6 +25,11 @@ SHAPES = [  # name, objects, k, m, sparsity, dependent fraction
     ("k128 sparse 0.9", 64, 128, 128, 0.9, 0.02),
     ("configs[4] share k128, LU (never leaves the clean state)", 512, 128, 128, -1.0, 0.0),
 ]
+if os.environ.get("ELIM_SHAPES") == "small":  # small-k crossover of the one-wave register kernel (path 4)
+    SHAPES = [("k8 x4096", 4096, 8, 8, 0.0, 0.0), ("k16 x4096", 4096, 16, 16, 0.0, 0.0),
+              ("k16 x512", 512, 16, 16, 0.0, 0.0), ("k16 m24 sparse 0.5 dep", 4096, 16, 24, 0.5, 0.1),
+              ("k24 x2048", 2048, 24, 24, 0.0, 0.0), ("k32 x1024", 1024, 32, 32, 0.0, 0.0),
+              ("k20 m40 x2048", 2048, 20, 40, 0.2, 0.05), ("k12 x4096", 4096, 12, 12, 0.0, 0.0)]
 
 
 def gf_mul_table():

@@ -780,3 +780,25 @@ def test_large_piece_count_recode(ctx, orc, k, n, count):
     got = host(out)[0]
     for c in range(count):
         assert np.array_equal(got[c], orc.recode(pieces, k + L, k, r[0, c])), c
+
+
+@pytest.mark.parametrize("k,m,sparsity,dep", [(16, 16, 0.0, 0.0), (16, 24, 0.5, 0.1), (8, 12, 0.7, 0.1)])
+def test_decode_many_small_objects(ctx, k, m, sparsity, dep):
+    """2,048 objects with k <= 16: the default path takes the one-wave register kernel (rref.hip `small_many`);
+    every object's statuses and payload rows against the oracle."""
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(2048 + k * 3 + m)
+    nobj, L = 2048, 8
+    seqs = _sequences(rng, nobj, k, m, L, sparsity, dep)
+    decoded = dev(np.zeros((nobj, k, L), np.uint8))
+    pst, ost, dl = batch.decode_batch(dev(seqs), k, decoded, ctx)
+    got = host(decoded)
+    for o in range(nobj):
+        od = OracleDecoder(L, k)
+        want = [S[od.decode(p)] for p in seqs[o]]
+        assert [S[x] for x in pst[o]] == want, o
+        pay = od.padded_payload()
+        assert np.array_equal(got[o, : pay.shape[0]], pay), o
+        st, _ = od.get_decoded_data()
+        assert S[ost[o]] == S[st], o
