@@ -1,7 +1,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT}"
 for pass in 1 2; do
-  for v in 8 7 9; do
+  for v in ${VARIANTS:-8 7 9}; do
     VARIANT=$v timeout -k 10 300 python scripts/bench_configs.py > gpurun_out/v_$v.jsonl 2>/dev/null || { echo "v=$v failed"; exit 1; }
     python -c "
 import json
