@@ -222,6 +222,88 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_perm_kernel(MatmulParams p
     copy_header(p, t);
 }
 
+// Narrow operands (< one 4 KiB column block: the ragged k + L tail of a recode, small pieces).  The work is a
+// chain over the sources, so it is latency-bound: one workgroup per (object, NT-row tile) builds the tables of ALL
+// its (source, row) coefficients at once (one barrier, no per-chunk rebuild), then each lane walks the sources
+// with PF source rows in flight; full 16-byte slots load and store as vectors (AL), the last partial one bytewise.
+// (The perm kernel it replaces here -- two rows in flight, tables per 32-source chunk -- took 91 us for configs[3]'s
+// 64-byte tail: profiles/r02_narrow_ab.txt.)
+template <int NT, bool AL>
+__global__ __launch_bounds__(kThreads) void gf_matmul_narrow_kernel(MatmulParams p, int row_tiles) {
+    extern __shared__ uint4 narrow_lds[];  // [n_in][NT] of (t0lo, t0hi, t1lo, t1hi), then [n_in][NT] of t2
+    constexpr int PF = 8;
+    const int rt = int(blockIdx.x) % row_tiles, obj = int(blockIdx.x) / row_tiles;
+    const int row0 = rt * NT, rows_here = min(NT, p.n_out - row0);
+    uint4 *t01 = narrow_lds;
+    uint32_t *t2 = reinterpret_cast<uint32_t *>(narrow_lds + p.n_in * NT);
+    const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
+    for (int e = threadIdx.x; e < p.n_in * NT; e += kThreads) {
+        const int i = e % NT, j = e / NT;
+        const PermTable pt = make_perm_table(i < rows_here ? coef_base[int64_t(i) * p.coef_row + j] : uint8_t(0));
+        t01[e] = make_uint4(pt.t0lo, pt.t0hi, pt.t1lo, pt.t1hi);
+        t2[e] = pt.t2;
+    }
+    if (p.hdr != nullptr) {  // coded-piece header (encoder.rs:246-248) when the whole product is narrow
+        uint8_t *h = p.hdr + int64_t(obj) * p.hdr_obj + int64_t(row0) * p.hdr_row;
+        for (int e = threadIdx.x; e < rows_here * p.n_in; e += kThreads) {
+            const int i = e / p.n_in, j = e % p.n_in;
+            h[int64_t(i) * p.hdr_row + j] = coef_base[int64_t(i) * p.coef_row + j];
+        }
+    }
+    __syncthreads();
+    for (int64_t col = int64_t(threadIdx.x) * kBytesPerThread; col < p.width; col += int64_t(kColBlock)) {
+        const int nbytes = int(min<int64_t>(kBytesPerThread, p.width - col));
+        const uint8_t *in = p.in + int64_t(obj) * p.in_obj + col;
+        uint32_t acc[NT][4];
+#pragma unroll
+        for (int i = 0; i < NT; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0u;
+        for (int j0 = 0; j0 < p.n_in; j0 += PF) {
+            uint4 x[PF];
+#pragma unroll
+            for (int u = 0; u < PF; ++u) x[u] = load16<AL>(in + int64_t(min(j0 + u, p.n_in - 1)) * p.in_row, nbytes);
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                const int j = j0 + u;
+                if (j >= p.n_in) break;
+                const Sel a = selectors(x[u]);
+#pragma unroll
+                for (int i = 0; i < NT; ++i) {
+                    const uint4 ta = t01[j * NT + i];
+                    const uint32_t ta2 = t2[j * NT + i];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        acc[i][q] = xor3(xor3(acc[i][q], vperm(ta.y, ta.x, a.s0[q]), vperm(ta.w, ta.z, a.s1[q])),
+                                         vperm(ta2, ta2, a.s2[q]), 0u);
+                }
+            }
+        }
+        uint8_t *out = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + col;
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+            if (i < rows_here)
+                store16<AL>(out + int64_t(i) * p.out_row, make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]),
+                            nbytes);
+    }
+}
+
+constexpr int kNarrowRows = 4;
+inline size_t narrow_lds_bytes(int n_in) { return size_t(n_in) * kNarrowRows * 20; }
+constexpr size_t kNarrowMaxLds = 64 * 1024;
+
+hipError_t launch_narrow(const MatmulParams &p, bool aligned, hipStream_t s) {
+    const int row_tiles = (p.n_out + kNarrowRows - 1) / kNarrowRows;
+    const int64_t total = int64_t(p.n_obj) * row_tiles;
+    if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    const size_t lds = narrow_lds_bytes(p.n_in);
+    if (aligned)
+        hipLaunchKernelGGL((gf_matmul_narrow_kernel<kNarrowRows, true>), dim3(unsigned(total)), dim3(kThreads), lds, s,
+                           p, row_tiles);
+    else
+        hipLaunchKernelGGL((gf_matmul_narrow_kernel<kNarrowRows, false>), dim3(unsigned(total)), dim3(kThreads), lds, s,
+                           p, row_tiles);
+    return hipGetLastError();
+}
+
 // Streaming variant for few output rows (n_out <= 3: one coded piece per pass is HBM-bound, ~1 multiply-add
 // per source byte read): the perm kernel's arithmetic with PF source rows in flight per lane (it keeps one
 // row pair), loaded non-temporally (each source byte is read once).  Whole aligned 4 KiB blocks only.
@@ -396,6 +478,15 @@ hipError_t launch_stream3(const MatmulParams &q, int row_tiles, int col_blocks, 
     hipLaunchKernelGGL((gf_matmul_stream3_kernel<NT, PF, VW, SH64>), dim3(unsigned(total)), dim3(kThreads), 0, s, q,
                        row_tiles, col_blocks / VW);
     return hipGetLastError();
+}
+
+// Narrow-operand kernel (A/B knob, read once): RLNC_NARROW = 0 takes the round-1 perm path (two rows per workgroup)
+int narrow_form() {
+    static const int f = [] {
+        const char *e = getenv("RLNC_NARROW");
+        return e ? atoi(e) : 1;
+    }();
+    return f;
 }
 
 // Single-pass stream kernel form; RLNC_STREAM_FORM (A/B knob, read once): 0 = gf_matmul_stream_kernel<NT, 2>,
@@ -1409,7 +1500,11 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
     if (v == MatmulVariant::Wide || v == MatmulVariant::Wide4) v = MatmulVariant::Perm;
     // narrow (< one 4 KiB column block, e.g. the ragged tail of a recode over k + L bytes): the work is the
     // sources x rows chain of one block, so split the rows over many workgroups (2 rows each)
-    if (p.width < kColBlock && p.n_out > 2) return launch_nt<2>(p, s, v, aligned);
+    if (p.width < kColBlock && p.n_out > 2) {
+        if (v == MatmulVariant::Perm && narrow_lds_bytes(p.n_in) <= kNarrowMaxLds && narrow_form() == 1)
+            return launch_narrow(p, aligned, s);
+        return launch_nt<2>(p, s, v, aligned);
+    }
     if (p.n_out <= 1) return launch_nt<1>(p, s, v, aligned);
     if (p.n_out <= 2) return launch_nt<2>(p, s, v, aligned);
     if (p.n_out <= 4) return launch_nt<4>(p, s, v, aligned);
