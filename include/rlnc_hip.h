@@ -112,32 +112,26 @@ int rlnc_gf256_matmul(rlnc_context *ctx, const rlnc_matmul_desc *desc);
 /* Kernel variant of the GF(2^8) matmul (all bit-identical; the switch exists for A/B measurement):
  *   0 = perm       3-bit split tables in LDS consumed by v_perm_b32
  *   1 = nibble     the reference's 4-bit LOW/HIGH tables looked up from LDS byte-wise (ablation)
- *   2 = perm3      three sources per step: 24 bits in eight 3-bit chunks, tables pre-summed
- *   3 = wide2, 4 = wide4   perm with 2 / 4 column slots per lane
- *   5 = bitsliced  bit-plane transpose + register-indexed XOR of plane combinations (full 16 KiB column
- *                  blocks of 16-byte-aligned operands with >= 4 output rows; the rest goes to perm)
- *   6 = bitsliced-jump  as 5, but each (row, source) is one call into a code block specialised for the
- *                  coefficient (16 v_bitop3_b32 XOR3s of plane combinations)
+ *   6 = bitsliced-jump  bit-plane transpose; each (row, source) is one call into a code block specialised for the
+ *                  coefficient (16 v_bitop3_b32 XOR3s of plane combinations); full 4 KiB column blocks of 16-byte
+ *                  aligned operands with >= 4 output rows, the rest goes to perm
  *   7 = bitsliced-jump-shared  as 6; in 32-row tiles each of the 4 waves builds one quarter of every source
  *                  row's plane combinations and the quarters are exchanged through LDS
  *   8 = bitsliced-jump-shared-8w  as 7; above 32 output rows, 64-row tiles of 8 waves (one workgroup per CU):
  *                  waves 0-3 stage the source and build the combinations three rows ahead, waves 4-7 only
  *                  read them and call; a barrier every third row -- the default
- *   9 = bitsliced-jump-run  as 8, with column runs: above 32 output rows a workgroup walks up to 8 consecutive
- *                  4 KiB column blocks of one object, its source-row stream (DMA, staging, combinations, block
- *                  addresses) unbroken across them, so only a run's first block pays the prologue (5 % faster
- *                  for an isolated large launch, not beside other launches)
+ * Other values fail with RLNC_ERR_INVALID_ARGUMENT, except in the diagnostic A/B build (make -C rlnc_amd/csrc ab:
+ * librlnc_hip_ab.so), which keeps the measured history: 2 perm3, 3/4 wide2/wide4, 5 bitsliced with
+ * register-indexed XORs, 9 column runs.
  * max_tile_rows caps the output rows per launch/workgroup (0 = automatic, else 1/2/4/8/16/32). */
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows);
-/* Column blocks per workgroup of variant 9 (0 = automatic: enough runs for >= 4 workgroups per CU, at most 8;
- * else 1..64).  A tuning and test knob; results are bit-identical for every value. */
+/* Column blocks per workgroup of variant 9 (A/B build only; 0 = automatic, else 1..64).  Bit-identical for every
+ * value. */
 int rlnc_set_column_run(rlnc_context *ctx, int col_run);
 /* Where rlnc_decode_batch runs the coefficient elimination: 0 = auto (device when it fits LDS, default),
- * 1 = host threads, 2 = device, 3 = device with the clean-state steps on LDS instead of registers, 4 = device
- * with the clean-state steps on one wave's registers, 5 = device, blocked clean run (up to 16 pieces per step,
- * 4 waves per object; k + m <= 256 -- what 0 and 2 use when it applies), 6 = device, the round-1 register path
- * (initial clean run over 4 waves when k <= 64).
- * All are exact replicas; the switch exists for A/B tests. */
+ * 1 = host threads, 2 = device, 5 = device, blocked clean run (k + m <= 256, else RLNC_ERR_INVALID_ARGUMENT; what 0
+ * and 2 use when it applies).  The A/B build adds 3 (clean state on LDS), 4 (one wave's registers) and 6 (the
+ * round-1 multi-wave register path).  All are exact replicas; the switch exists for A/B tests. */
 int rlnc_set_decode_path(rlnc_context *ctx, int path);
 
 /* ---- Encoder: src/full/encoder.rs ----------------------------------------------------------------- */
@@ -278,9 +272,12 @@ int rlnc_pad_batch_device(rlnc_context *ctx, const rlnc_pad_desc *descs, size_t 
 /* Encoder::new from a device byte string: the encoder owns its padded image (built on the device). */
 int rlnc_encoder_new_device(rlnc_context *ctx, const uint8_t *data_dev, size_t data_len, size_t piece_count,
                             rlnc_encoder **out);
-/* A ragged batch: every object with its own k, L, n and buffers (device pointers; strides 0 = dense), n coded
- * pieces coeffs ‖ data each (encoder.rs:241-250).  Objects of one shape whose buffers sit at a constant object
- * stride share a launch.  Asynchronous on the context stream. */
+/* Ragged batches: every object with its own shape and buffers (device pointers; strides 0 = dense), as a sender or
+ * receiver holding pieces of many objects has them.  Each kernel stage is one launch over a device-side descriptor
+ * table, whatever the number of objects and shapes (the matmul stage: <= 4 launches -- block addresses, the
+ * bit-sliced program for <= 32 and > 32 output rows, the perm kernel for < 4 KiB tails and unaligned operands).
+ * Asynchronous on the context stream.  Error checks run over all descriptors before anything is launched.
+ * rlnc_encode_ragged: n coded pieces coeffs ‖ data per object (encoder.rs:241-250 × n). */
 typedef struct rlnc_object_desc {
     const uint8_t *src;      /* k source pieces of L bytes */
     size_t src_row_stride;   /* >= L, 0 = L */
@@ -290,6 +287,32 @@ typedef struct rlnc_object_desc {
     size_t k, L, n;
 } rlnc_object_desc;
 int rlnc_encode_ragged(rlnc_context *ctx, const rlnc_object_desc *objs, size_t count);
+/* Recoder::recode_with_buf (recoder.rs:122-153) × n_recoded per object: out[i] = Σ_j r[i][j] · pieces[j] over the
+ * full pieces (coefficient header and data are one linear map).  Checks in Recoder::new's order (recoder.rs:69-80):
+ * n == 0 NotEnoughPiecesToRecode, k + L == 0 PieceLengthZero, k == 0 PieceCountZero, L == 0 PieceLengthTooShort. */
+typedef struct rlnc_recode_object_desc {
+    const uint8_t *pieces;   /* n received full pieces of k + L bytes */
+    size_t piece_row_stride; /* >= k + L, 0 = k + L */
+    const uint8_t *r;        /* n_recoded × n recoding coefficients (rng.fill_bytes draws them, recoder.rs:131) */
+    uint8_t *out;            /* n_recoded full recoded pieces */
+    size_t out_row_stride;   /* >= k + L, 0 = k + L */
+    size_t k, L, n, n_recoded;
+} rlnc_recode_object_desc;
+int rlnc_recode_ragged(rlnc_context *ctx, const rlnc_recode_object_desc *objs, size_t count);
+/* Decoder::decode for pieces 0..m-1 of every object + get_decoded_data (decoder.rs:96-177), like
+ * rlnc_decode_batch_device per object: decoded [k][L] (padded payload rows in the reference's row order),
+ * piece_status_dev int32 [Σ m] (object order, each object's m statuses of its decode() calls), object_status_dev
+ * int32 [count] (Ok / NotAllPiecesReceivedYet / InvalidDecodedDataFormat), data_len_dev int64 [count] (unpadded
+ * length when Ok).  The exact elimination runs on the device when an object's [coeffs | E] fits LDS, else on host
+ * threads (then the call is not capturable).  L == 0 PieceLengthZero, k == 0 PieceCountZero (decoder.rs:66-71). */
+typedef struct rlnc_decode_object_desc {
+    const uint8_t *pieces;   /* m received full pieces, coeffs ‖ data */
+    size_t piece_row_stride; /* >= k + L, 0 = k + L */
+    uint8_t *decoded;        /* k × L bytes */
+    size_t k, L, m;
+} rlnc_decode_object_desc;
+int rlnc_decode_ragged(rlnc_context *ctx, const rlnc_decode_object_desc *objs, size_t count, int32_t *piece_status_dev,
+                       int32_t *object_status_dev, int64_t *data_len_dev);
 
 /* ---- host-resident pieces (a socket or a file) ---------------------------------------------
  * The batch API above for host buffers: objects stream through the device in windows of `window` objects (0 =

@@ -30,6 +30,17 @@ class ObjectDesc(C.Structure):
                 ("piece_row_stride", C.c_size_t), ("k", C.c_size_t), ("L", C.c_size_t), ("n", C.c_size_t)]
 
 
+class RecodeObjDesc(C.Structure):
+    _fields_ = [("pieces", C.c_void_p), ("piece_row_stride", C.c_size_t), ("r", C.c_void_p), ("out", C.c_void_p),
+                ("out_row_stride", C.c_size_t), ("k", C.c_size_t), ("L", C.c_size_t), ("n", C.c_size_t),
+                ("n_recoded", C.c_size_t)]
+
+
+class DecodeObjDesc(C.Structure):
+    _fields_ = [("pieces", C.c_void_p), ("piece_row_stride", C.c_size_t), ("decoded", C.c_void_p), ("k", C.c_size_t),
+                ("L", C.c_size_t), ("m", C.c_size_t)]
+
+
 class MatmulDesc(C.Structure):
     _fields_ = [
         ("in_", C.c_void_p), ("in_obj_stride", C.c_int64), ("in_row_stride", C.c_int64),
@@ -110,6 +121,8 @@ _SIGS = {
     "rlnc_pad_batch_device": (C.c_int, [vp, vp, C.c_size_t]),
     "rlnc_encoder_new_device": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.POINTER(vp)]),
     "rlnc_encode_ragged": (C.c_int, [vp, vp, C.c_size_t]),
+    "rlnc_recode_ragged": (C.c_int, [vp, vp, C.c_size_t]),
+    "rlnc_decode_ragged": (C.c_int, [vp, vp, C.c_size_t, vp, vp, vp]),
     "rlnc_encode_host_stream": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, vp, C.c_size_t, vp,
                                           C.c_size_t]),
     "rlnc_decode_host_stream": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp,

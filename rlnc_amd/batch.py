@@ -27,8 +27,11 @@ def _ctx_for(t, ctx: Context | None) -> Context:
 
     dev = t.device.index or 0
     if ctx is None:
-        return stream_context(dev, torch.cuda.current_stream(dev).cuda_stream)
-    ctx.use_torch_stream()
+        ctx = stream_context(dev, torch.cuda.current_stream(dev).cuda_stream)
+    else:
+        ctx.use_torch_stream()
+    if torch.cuda.is_current_stream_capturing():
+        ctx.graph_bound = True  # the graph holds its workspace addresses: never evicted (context.stream_context)
     return ctx
 
 
@@ -205,3 +208,79 @@ def mul_vec_by_scalar_then_add_into_vec(dst, src, scalar: int, ctx: Context | No
     check(ctx.lib.rlnc_gf256_mul_vec_by_scalar_then_add_into_vec(ctx.h, C.c_void_p(dst.data_ptr()),
                                                                  C.c_void_p(src.data_ptr()), dst.numel(), scalar),
           ctx.lib)
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# ragged batches (include/rlnc_hip.h: rlnc_encode_ragged / rlnc_recode_ragged / rlnc_decode_ragged): objects of
+# different shapes and buffers, one launch per kernel stage
+# ------------------------------------------------------------------------------------------------------------------
+def _rows(t):
+    """(pointer, row stride) of a 2-D uint8 device view whose rows are contiguous."""
+    import torch
+
+    assert t.is_cuda and t.dtype == torch.uint8 and t.dim() == 2 and (t.shape[1] <= 1 or t.stride(1) == 1)
+    return t.data_ptr(), (t.stride(0) if t.shape[0] > 1 else t.shape[1])
+
+
+def encode_ragged(objs, ctx: Context | None = None) -> None:
+    """objs: (src [k][L], coeffs [n][k], pieces [n][k+L]) per object -> n coded pieces coeffs ‖ data each."""
+    from ._lib import ObjectDesc
+
+    if not objs:
+        return
+    ctx = _ctx_for(objs[0][0], ctx)
+    descs = []
+    for src, co, pc in objs:
+        k, L = src.shape
+        n = co.shape[0]
+        assert tuple(co.shape) == (n, k) and tuple(pc.shape) == (n, k + L) and co.is_contiguous()
+        sp, ss = _rows(src)
+        pp, ps = _rows(pc)
+        descs.append(ObjectDesc(sp, ss, co.data_ptr(), pp, ps, k, L, n))
+    arr = (ObjectDesc * len(descs))(*descs)
+    check(ctx.lib.rlnc_encode_ragged(ctx.h, arr, len(descs)), ctx.lib)
+
+
+def recode_ragged(objs, ctx: Context | None = None) -> None:
+    """objs: (pieces [n][k+L], r [count][n], out [count][k+L], k) per object (recoder.rs:122-153 × count)."""
+    from ._lib import RecodeObjDesc
+
+    if not objs:
+        return
+    ctx = _ctx_for(objs[0][0], ctx)
+    descs = []
+    for pieces, r, out, k in objs:
+        n, full = pieces.shape
+        count = r.shape[0]
+        assert tuple(r.shape) == (count, n) and r.is_contiguous() and tuple(out.shape) == (count, full)
+        pp, ps = _rows(pieces)
+        op, os_ = _rows(out)
+        descs.append(RecodeObjDesc(pp, ps, r.data_ptr(), op, os_, k, full - k, n, count))
+    arr = (RecodeObjDesc * len(descs))(*descs)
+    check(ctx.lib.rlnc_recode_ragged(ctx.h, arr, len(descs)), ctx.lib)
+
+
+def decode_ragged(objs, ctx: Context | None = None):
+    """objs: (pieces [m][k+L], k, decoded [k][L]) per object.  Returns device tensors (piece_status int32 [sum m]
+    in object order, object_status int32 [count], data_len int64 [count]); asynchronous like decode_batch_device."""
+    import torch
+
+    from ._lib import DecodeObjDesc
+
+    dev = objs[0][0].device
+    ctx = _ctx_for(objs[0][0], ctx)
+    descs = []
+    for pieces, k, dec in objs:
+        m, full = pieces.shape
+        L = full - k
+        assert tuple(dec.shape) == (k, L) and dec.is_contiguous()
+        pp, ps = _rows(pieces)
+        descs.append(DecodeObjDesc(pp, ps, dec.data_ptr(), k, L, m))
+    total_m = sum(d.m for d in descs)
+    ps_t = torch.empty(total_m, dtype=torch.int32, device=dev)
+    os_t = torch.empty(len(descs), dtype=torch.int32, device=dev)
+    dl_t = torch.empty(len(descs), dtype=torch.int64, device=dev)
+    arr = (DecodeObjDesc * len(descs))(*descs)
+    check(ctx.lib.rlnc_decode_ragged(ctx.h, arr, len(descs), C.c_void_p(ps_t.data_ptr()), C.c_void_p(os_t.data_ptr()),
+                                     C.c_void_p(dl_t.data_ptr())), ctx.lib)
+    return ps_t, os_t, dl_t

@@ -19,6 +19,7 @@ class Context:
         check(self.lib.rlnc_context_create(int(device), C.byref(h)), self.lib)
         self.h = h
         self.device = int(device)
+        self.graph_bound = False  # set when a call on it was captured into a HIP graph (batch._ctx_for)
 
     def close(self):
         if getattr(self, "h", None):
@@ -47,18 +48,17 @@ class Context:
         check(self.lib.rlnc_context_synchronize(self.h), self.lib)
 
     def set_decode_path(self, path: int = 0):
-        """0 auto, 1 host elimination, 2 device elimination, 3 device with the clean state on LDS, 4 device on
-        one wave's registers, 5 device blocked clean run (what 0/2 use when k + m <= 256), 6 device, the round-1
-        multi-wave register path (all exact; 2-6 exist for A/B)."""
+        """0 auto, 1 host elimination, 2 device elimination, 5 device blocked clean run (what 0/2 use when
+        k + m <= 256; InvalidArgument when it does not apply).  The diagnostic A/B build (make -C rlnc_amd/csrc ab)
+        adds 3 (clean state on LDS), 4 (one wave's registers) and 6 (the round-1 multi-wave register path).  All
+        are exact."""
         check(self.lib.rlnc_set_decode_path(self.h, int(path)), self.lib)
 
     def set_kernel_variant(self, variant: int = 8, max_tile_rows: int = 0):
-        """GF(2^8) matmul variant (include/rlnc_hip.h): 7 = bit-sliced, one code block per coefficient, plane
-        combinations built once per workgroup and shared through LDS, 6 = the same without sharing,
-        5 = bit-sliced with register-indexed XORs, 0 = perm, 1 = nibble (the reference's 4-bit tables,
-        ablation), 2 = perm3, 3/4 = wide2/wide4, 8 = as 7 with 64-row tiles of 8 waves above 32 output rows
-        (waves 4-7 only read the shared combinations; a barrier every third row; the default), 9 = as 8 with
-        column runs (a workgroup walks up to 8 column blocks, one prologue per run).  All are bit-identical."""
+        """GF(2^8) matmul variant (include/rlnc_hip.h): 8 = bit-sliced, one code block per coefficient, plane
+        combinations built once per workgroup and shared through LDS, 64-row tiles of 8 waves above 32 output
+        rows (the default); 7 = the same with 32-row tiles; 6 = without sharing; 0 = perm; 1 = nibble (the
+        reference's 4-bit tables, ablation).  The diagnostic A/B build adds 2-5 and 9.  All are bit-identical."""
         check(self.lib.rlnc_set_kernel_variant(self.h, int(variant), int(max_tile_rows)), self.lib)
 
     def set_column_run(self, col_run: int = 0):
@@ -75,17 +75,40 @@ def default_context(device: int = 0) -> Context:
     return ctxs[device]
 
 
+# Per-thread cap on the stream-bound default contexts.  Each context owns grow-only workspaces, so code rotating
+# through torch's stream pool (up to 32 streams per priority) would otherwise keep one full workspace set per stream
+# alive.  The least recently used context is closed beyond the cap (its stream is synchronised first, and objects
+# built on it keep their own reference) -- unless a HIP graph captured a call on it: the graph holds that context's
+# workspace addresses, so it is never evicted.
+STREAM_CONTEXTS_PER_THREAD = 4
+
+
 def stream_context(device: int, stream_handle: int) -> Context:
-    """This thread's context bound to one HIP stream (created on first use and kept)."""
+    """This thread's context bound to one HIP stream (created on first use; at most STREAM_CONTEXTS_PER_THREAD
+    are kept per thread, least recently used first out, graph-bound ones never)."""
+    from collections import OrderedDict
+
     ctxs = getattr(_tls, "sctxs", None)
     if ctxs is None:
-        ctxs = _tls.sctxs = {}
+        ctxs = _tls.sctxs = OrderedDict()
     key = (device, int(stream_handle or 0))
     c = ctxs.get(key)
     if c is None:
         c = ctxs[key] = Context(device)
         c.set_stream(key[1])
+        evictable = [k for k, v in ctxs.items() if k != key and not v.graph_bound]
+        while len(ctxs) > STREAM_CONTEXTS_PER_THREAD and evictable:
+            ctxs.pop(evictable.pop(0)).close()
+    else:
+        ctxs.move_to_end(key)
     return c
 
 
-__all__ = ["Context", "default_context", "stream_context", "RLNCError"]
+def release_stream_contexts() -> None:
+    """Close this thread's stream-bound default contexts (except graph-bound ones)."""
+    ctxs = getattr(_tls, "sctxs", None) or {}
+    for k in [k for k, v in ctxs.items() if not v.graph_bound]:
+        ctxs.pop(k).close()
+
+
+__all__ = ["Context", "default_context", "stream_context", "release_stream_contexts", "RLNCError"]

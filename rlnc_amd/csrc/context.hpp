@@ -145,9 +145,13 @@ struct rlnc_context {
     };
     std::vector<std::unique_ptr<HsSlot>> hs_slots;
     hipStream_t hs_h2d = nullptr, hs_d2h = nullptr;
-    DevBuf ws_tab;  // descriptor tables of the wire-format calls (wire.hip), uploaded from pin_tab
+    DevBuf ws_tab;  // descriptor tables of the wire-format / ragged calls (wire.hip), uploaded from pin_tab
     PinBuf pin_tab;
     hipEvent_t tab_ev = nullptr;  // the last descriptor upload (pin_tab may be rewritten once it has run)
+    // descriptor tables of calls captured into HIP graphs: bump-allocated, never reused or moved (a replay rewrites
+    // exactly its captured bytes); reserved by eager calls, since nothing may be allocated inside a capture
+    std::vector<std::unique_ptr<DevBuf>> cap_arenas;
+    size_t cap_used = 0;
 
     void retain() { refs.fetch_add(1, std::memory_order_relaxed); }
     void release() {

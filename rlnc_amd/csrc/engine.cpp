@@ -231,15 +231,28 @@ int rlnc_context_synchronize(rlnc_context *ctx) {
     return RLNC_OK;
 }
 
+// Shipped decode paths: 0 auto, 1 host, 2 device, 5 device blocked run; 3, 4 and 6 (the round-1 LDS / register
+// forms) exist in diagnostic builds only (make -C rlnc_amd/csrc ab: -DRLNC_AB_VARIANTS).
 int rlnc_set_decode_path(rlnc_context *ctx, int path) {
+#ifdef RLNC_AB_VARIANTS
     CHECK_ARG(ctx != nullptr && path >= 0 && path <= 6);
+#else
+    CHECK_ARG(ctx != nullptr && (path == 0 || path == 1 || path == 2 || path == 5));
+#endif
     ctx->decode_path = path;
     return RLNC_OK;
 }
 
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows) {
     CHECK_ARG(ctx != nullptr);
+#ifdef RLNC_AB_VARIANTS
     CHECK_ARG(variant >= 0 && variant <= 9);
+#else
+    // shipped: 0 perm, 1 nibble (the reference's tables, ablation), 6 (the unshared bit-sliced program, which also
+    // serves <= 16-row products and a first use inside a graph capture), 7 and 8 (the bit-sliced default); 2-5 and 9
+    // are the A/B history, in diagnostic builds only
+    CHECK_ARG(variant == 0 || variant == 1 || variant == 6 || variant == 7 || variant == 8);
+#endif
     CHECK_ARG(max_tile_rows == 0 || max_tile_rows == 1 || max_tile_rows == 2 || max_tile_rows == 4 ||
               max_tile_rows == 8 || max_tile_rows == 16 || max_tile_rows == 32);
     ctx->variant = static_cast<rlnc::MatmulVariant>(variant);
@@ -878,6 +891,8 @@ static int decode_eliminate_impl(rlnc_context *ctx, const uint8_t *pieces, size_
     rp.status = pstat_dev;
     rp.rank = rank_dev;
     rp.lds_only = ctx->decode_path == 3 ? 1 : ctx->decode_path == 4 ? 2 : ctx->decode_path == 5 ? 3 : ctx->decode_path == 6 ? 4 : 0;
+    if (ctx->decode_path == 5 && !rlnc::rref_block_eligible(int(k), int(m)))  // no silent fallback to another kernel
+        return set_error(RLNC_ERR_INVALID_ARGUMENT, "decode path 5 (blocked run) needs k + m <= 256 (k=%zu, m=%zu)", k, m);
     HIP_TRY(rlnc::launch_rref_batch(rp, ctx->stream));
     return RLNC_OK;
 }

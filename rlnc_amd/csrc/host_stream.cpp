@@ -35,13 +35,28 @@ int num_slots() {
     return n;
 }
 
-bool is_pinned(const void *p) {
+// What a host-stream buffer [p, p + bytes) is: 1 = pinned over the whole range (hipHostMalloc, or hipHostRegister
+// covering it: copied by DMA directly), 0 = pageable (staged through pinned buffers by host threads), -1 = device
+// memory (a misuse: the host threads would fault on it).  A registration that covers only the start of the range, or
+// whose extent cannot be read, counts as pageable: the staged copy is always correct for host memory.
+int host_kind(const void *p, size_t bytes) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();  // clear the sticky "invalid value" of an unregistered pointer
-        return false;
+        return 0;
     }
-    return a.type == hipMemoryTypeHost;
+    if (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeArray) return -1;
+    if (a.type != hipMemoryTypeHost) return 0;
+    // the registered allocation must cover the whole range
+    void *base = nullptr;
+    size_t size = 0;
+    const void *dp = a.devicePointer ? a.devicePointer : p;
+    if (hipMemGetAddressRange(&base, &size, const_cast<void *>(dp)) != hipSuccess || base == nullptr) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    const uintptr_t off = reinterpret_cast<uintptr_t>(dp) - reinterpret_cast<uintptr_t>(base);
+    return off <= size && bytes <= size - off ? 1 : 0;
 }
 
 // memcpy of `rows` rows of `width` bytes (strides in bytes) on up to 16 host threads
@@ -165,7 +180,10 @@ int rlnc_encode_host_stream(rlnc_context *ctx, const uint8_t *src, size_t k, siz
     int st = ctx->activate();
     if (st) return st;
     const size_t full = k + L, in_b = k * L, co_b = n * k, out_b = n * full;
-    const bool pin_in = is_pinned(src) && is_pinned(coeffs), pin_out = is_pinned(pieces);
+    const int ks = host_kind(src, nobj * in_b), kc = host_kind(coeffs, nobj * co_b), kp = host_kind(pieces, nobj * out_b);
+    if (ks < 0 || kc < 0 || kp < 0)
+        return set_error(RLNC_ERR_INVALID_ARGUMENT, "host-stream buffers must be host memory (got a device pointer)");
+    const bool pin_in = ks == 1 && kc == 1, pin_out = kp == 1;
     Pipeline pl(ctx);
     if ((st = pl.init())) return st;
     const size_t W = window ? std::min(window, nobj) : auto_window(in_b, nobj, pl.n);
@@ -234,7 +252,10 @@ int rlnc_decode_host_stream(rlnc_context *ctx, const uint8_t *pieces, size_t obj
     const bool dev_elim = rlnc::rref_lds_bytes(int(k), int(m)) <= rlnc::kRrefMaxLds && ctx->decode_path != 1;
     int st = ctx->activate();
     if (st) return st;
-    const bool pin_in = is_pinned(pieces), pin_out = is_pinned(decoded);
+    const int kin = host_kind(pieces, (nobj - 1) * obj_stride + in_b), kout = host_kind(decoded, nobj * out_b);
+    if (kin < 0 || kout < 0)
+        return set_error(RLNC_ERR_INVALID_ARGUMENT, "host-stream buffers must be host memory (got a device pointer)");
+    const bool pin_in = kin == 1, pin_out = kout == 1;
     const size_t st_b = 8 + m * 4 + 4;  // per object: length (int64, first: aligned), piece statuses, object status
     Pipeline pl(ctx);
     if ((st = pl.init())) return st;

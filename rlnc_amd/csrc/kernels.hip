@@ -507,12 +507,14 @@ hipError_t launch_stream(const MatmulParams &p, int64_t full, hipStream_t s) {
     const int col_blocks = int(full / kColBlock);
     if (p.n_in <= kKC) {
         switch (stream_form()) {
+            case 11: return launch_stream3<NT, 1, 2, true>(q, row_tiles, col_blocks, s);
+#ifdef RLNC_AB_VARIANTS  // the other measured forms (profiles/r02_stream_ab.txt), diagnostic builds only
             case 8: return launch_stream3<NT, 2, 1, true>(q, row_tiles, col_blocks, s);
             case 9: return launch_stream3<NT, 2, 2, true>(q, row_tiles, col_blocks, s);
             case 10: return launch_stream3<NT, 2, 2, false>(q, row_tiles, col_blocks, s);
-            case 11: return launch_stream3<NT, 1, 2, true>(q, row_tiles, col_blocks, s);
             case 12: return launch_stream3<NT, 3, 1, true>(q, row_tiles, col_blocks, s);
             case 13: return launch_stream3<NT, 2, 1, false>(q, row_tiles, col_blocks, s);
+#endif
             default: break;
         }
     }
@@ -526,6 +528,7 @@ hipError_t launch_stream(const MatmulParams &p, int64_t full, hipStream_t s) {
     return hipGetLastError();
 }
 
+#ifdef RLNC_AB_VARIANTS  // variants 2-4 (perm3, wide2, wide4): A/B history, diagnostic builds only
 // Wide variant: each lane owns VW 16-byte slots per source row (slot v at column v·4 KiB inside an
 // (VW·4 KiB) block), so every table read from LDS — the measured bottleneck of the VW = 1 kernel (a build
 // that reads one table set per source row ran 2.2× faster) — feeds VW× more multiply-adds.  Full aligned
@@ -740,6 +743,8 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_perm3_kernel(MatmulParams 
     copy_header(p, t);
 }
 
+#endif  // RLNC_AB_VARIANTS
+
 // Ablation baseline: the reference's 4-bit split (LOW/HIGH nibble tables, simd_mul_table.rs:36-80) in
 // LDS, one ds_read_u8 per nibble per byte per lane.
 template <int NT, bool ALIGNED>
@@ -817,9 +822,12 @@ hipError_t launch_one(const MatmulParams &p, int64_t width, hipStream_t s, Matmu
     MatmulParams q = p;
     q.width = width;
     const dim3 grid{unsigned(total)}, block{unsigned(kThreads)};
+#ifdef RLNC_AB_VARIANTS
     if (v == MatmulVariant::Perm3)
         hipLaunchKernelGGL((gf_matmul_perm3_kernel<NT, VEC>), grid, block, 0, s, q, row_tiles, col_blocks);
-    else if (v == MatmulVariant::NibbleLds)
+    else
+#endif
+    if (v == MatmulVariant::NibbleLds)
         hipLaunchKernelGGL((gf_matmul_nibble_kernel<NT, VEC>), grid, block, 0, s, q, row_tiles, col_blocks);
     else
         hipLaunchKernelGGL((gf_matmul_perm_kernel<NT, VEC>), grid, block, 0, s, q, row_tiles, col_blocks);
@@ -844,6 +852,7 @@ hipError_t launch_nt(const MatmulParams &p, hipStream_t s, MatmulVariant v, bool
     return launch_one<NT, false>(t, p.width - full, s, v);
 }
 
+#ifdef RLNC_AB_VARIANTS
 template <int NT, int VW>
 hipError_t launch_wide(const MatmulParams &p, int64_t full, hipStream_t s) {
     const int row_tiles = (p.n_out + NT - 1) / NT;
@@ -877,9 +886,12 @@ hipError_t launch_wide_split(const MatmulParams &p, hipStream_t s) {
     return launch_nt<NT>(t, s, MatmulVariant::Perm, true);
 }
 
+#endif  // RLNC_AB_VARIANTS
+
 inline bool al16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 inline bool al16(int64_t v) { return (v & 15) == 0; }
 
+#ifdef RLNC_AB_VARIANTS  // variant 5 (register-indexed XORs): A/B history, diagnostic builds only
 // ---------------------------------------------------------------------------------------------------
 // Bit-sliced variant (gen_bitslice.py has the full derivation).  Measured on gfx950: v_perm_b32 issues at
 // ~4.1 cycles/wave64, so the 3-perm lookup costs ~19 cycles per 32-bit multiply-add; GF(2^8) multiply by
@@ -986,6 +998,8 @@ hipError_t launch_bs(const MatmulParams &p, hipStream_t s, void *scratch, size_t
     return hipGetLastError();
 }
 
+#endif  // RLNC_AB_VARIANTS
+
 // ---------------------------------------------------------------------------------------------------
 // Bit-sliced variant with one code block per coefficient (gen_bsjump.py has the derivation): the (row,
 // source) work is a call into block c -- 16 v_bitop3_b32 XOR3s with the combination registers baked in and
@@ -1040,51 +1054,15 @@ __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, in
 // RUN (W = 8 only, variant 9): the workgroup walks `run` consecutive column blocks of one (object, row tile) --
 // the column-run program (RLNC_BSJ_ASM_W8R) carries the source-row stream across the tile boundaries, so only the
 // first tile pays the prologue (first DMAs, first sets); the grid is objects x row tiles x runs
-template <int W, bool SHARE = false, bool RUN = false>
-__global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const void *stream, int row_tiles,
-                                                               int col_blocks, uint64_t *probe, int run = 1,
-                                                               int guided_nl = -1) {
-    static_assert(!SHARE || W == 4 || W == 8, "the shared-set programs are generated for 4 and 8 waves");
-    // (a 4-wave run program measured no gain: two workgroups per CU already hide the 32-row tile's prologue,
-    // profiles/r02_run_ab.txt)
-    static_assert(!RUN || (W == 8 && SHARE), "the column-run program is generated for the 8-wave shared program");
+// The tile of one workgroup: output rows [rt * 8W, +8W) x column block cb of object obj (the uniform batch
+// kernel below and the ragged kernel both end here).
+template <int W, bool SHARE, bool RUN>
+__device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stream, int row_tiles, int rt, int cb,
+                                         int obj, uint32_t tiles, uint64_t *probe) {
     constexpr int kTileRows = kBsjWaveRows * W;
     // W = 8: one workgroup per CU, so a deeper ring and 2 BAR8 set slots (the builders run BAR8 rows ahead)
     __shared__ __attribute__((aligned(16))) uint8_t ring[(W == 8 ? RLNC_BSJ_SLOTS8 : RLNC_BSJ_SLOTS) * kBsjColBlock];
     __shared__ __attribute__((aligned(16))) uint8_t cset[SHARE ? (W == 8 ? RLNC_BSJ_CSET_BYTES8 : RLNC_BSJ_CSET_BYTES) : 16];
-    int rt, cb, obj;
-    uint32_t tiles = 1;
-    if constexpr (RUN) {
-        const int runs = (col_blocks + run - 1) / run;
-        int r;
-        if (guided_nl < 0) {
-            decode_block(p.n_obj * row_tiles * runs, row_tiles, runs, rt, r, obj);
-            cb = r * run;
-            tiles = uint32_t(__builtin_amdgcn_readfirstlane(min(run, col_blocks - cb)));
-        } else {
-            // guided runs (launch_bsj checked: run | col_blocks, 8 | the run units): XCD x = b & 7 owns run units
-            // [x·per, (x+1)·per) (rt fastest, as decode_block), its first guided_nl dispatched workgroups walk one
-            // unit each, the later ones one column block of the remaining units -- short workgroups last
-            const int per = (p.n_obj * row_tiles * runs) >> 3;
-            const int b = blockIdx.x, x = b & 7, i = b >> 3;
-            int u, c = 0;
-            if (i < guided_nl) {
-                u = x * per + i;
-                tiles = uint32_t(run);
-            } else {
-                const int j = i - guided_nl;
-                u = x * per + guided_nl + j / run;
-                c = j % run;
-            }
-            rt = u % row_tiles;
-            const int rest = u / row_tiles;
-            r = rest % runs;
-            obj = rest / runs;
-            cb = r * run + c;
-        }
-    } else {
-        decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
-    }
     const int row0 = rt * kTileRows;
     const int rows = min(kTileRows, p.n_out - row0);
     if (p.hdr != nullptr && cb == 0) {  // coded-piece header (encoder.rs:246-248), 64·W threads
@@ -1139,6 +1117,51 @@ __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, c
 #pragma clang diagnostic pop
 }
 
+
+template <int W, bool SHARE = false, bool RUN = false>
+__global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const void *stream, int row_tiles,
+                                                               int col_blocks, uint64_t *probe, int run = 1,
+                                                               int guided_nl = -1) {
+    static_assert(!SHARE || W == 4 || W == 8, "the shared-set programs are generated for 4 and 8 waves");
+    // (a 4-wave run program measured no gain: two workgroups per CU already hide the 32-row tile's prologue,
+    // profiles/r02_run_ab.txt)
+    static_assert(!RUN || (W == 8 && SHARE), "the column-run program is generated for the 8-wave shared program");
+    int rt, cb, obj;
+    uint32_t tiles = 1;
+    if constexpr (RUN) {
+        const int runs = (col_blocks + run - 1) / run;
+        int r;
+        if (guided_nl < 0) {
+            decode_block(p.n_obj * row_tiles * runs, row_tiles, runs, rt, r, obj);
+            cb = r * run;
+            tiles = uint32_t(__builtin_amdgcn_readfirstlane(min(run, col_blocks - cb)));
+        } else {
+            // guided runs (launch_bsj checked: run | col_blocks, 8 | the run units): XCD x = b & 7 owns run units
+            // [x·per, (x+1)·per) (rt fastest, as decode_block), its first guided_nl dispatched workgroups walk one
+            // unit each, the later ones one column block of the remaining units -- short workgroups last
+            const int per = (p.n_obj * row_tiles * runs) >> 3;
+            const int b = blockIdx.x, x = b & 7, i = b >> 3;
+            int u, c = 0;
+            if (i < guided_nl) {
+                u = x * per + i;
+                tiles = uint32_t(run);
+            } else {
+                const int j = i - guided_nl;
+                u = x * per + guided_nl + j / run;
+                c = j % run;
+            }
+            rt = u % row_tiles;
+            const int rest = u / row_tiles;
+            r = rest % runs;
+            obj = rest / runs;
+            cb = r * run + c;
+        }
+    } else {
+        decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    }
+    bsj_tile<W, SHARE, RUN>(p, stream, row_tiles, rt, cb, obj, tiles, probe);
+}
+
 // waves per workgroup: 8 output rows each, at most 4 (a 32-row tile), no more than the rows need
 inline int bsj_waves(int n_out) { return n_out <= 8 ? 1 : n_out <= 16 ? 2 : 4; }
 // wide = variant 8: 64-row tiles of 8 waves (shared program) above 32 output rows
@@ -1191,6 +1214,7 @@ static hipError_t bsj_shared_base(hipStream_t s, void *scratch, uint64_t &base) 
     return hipSuccess;
 }
 
+#ifdef RLNC_AB_VARIANTS  // variant 9 (column runs): A/B history, diagnostic builds only
 // Column blocks per workgroup of the column-run program: enough runs for >= 4 workgroups per CU, at most 8
 // blocks each (RLNC_BSJ_RUN = n forces n; A/B knob, read once)
 static int bsj_run_length(int64_t tiles, int col_blocks, int requested) {
@@ -1222,6 +1246,8 @@ static int bsj_guided_pct() {
     }();
     return pct;
 }
+
+#endif  // RLNC_AB_VARIANTS
 
 hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full,
                       bool share, bool wide, bool run) {
@@ -1262,6 +1288,7 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
     else if (W == 2)
         hipLaunchKernelGGL(gf_matmul_bsj_kernel<2>, dim3(unsigned(total)), dim3(128), 0, s, q, stream, row_tiles,
                            col_blocks, nullptr);
+#ifdef RLNC_AB_VARIANTS
     else if (W == 8 && run) {
         const int rl = bsj_run_length(total, col_blocks, p.col_run);
         const int64_t units = int64_t(p.n_obj) * row_tiles * ((col_blocks + rl - 1) / rl);
@@ -1277,7 +1304,9 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
             hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true, true>), dim3(unsigned(units)), dim3(512), 0, s, q,
                                stream, row_tiles, col_blocks, nullptr, rl, -1);
         }
-    } else if (W == 8)
+    }
+#endif
+    else if (W == 8)
         hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true>), dim3(unsigned(total)), dim3(512), 0, s, q, stream,
                            row_tiles, col_blocks, nullptr);
     else if (share)
@@ -1287,6 +1316,162 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
         hipLaunchKernelGGL(gf_matmul_bsj_kernel<4>, dim3(unsigned(total)), dim3(256), 0, s, q, stream, row_tiles,
                            col_blocks, nullptr);
     return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Ragged batches (wire.hip: rlnc_encode_ragged / rlnc_recode_ragged / rlnc_decode_ragged): objects of different
+// shapes and buffers in ONE launch per kernel stage, driven by a device-side descriptor table (RaggedObj).  A
+// workgroup finds its object by binary search over the objects' first workgroups (wg0), then runs exactly the tile
+// the uniform kernels run for that object.
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int ragged_find(const RaggedObj *objs, int n, int64_t w, bool by_idx) {
+    int lo = 0, hi = n - 1;  // the last object whose start is <= w (starts ascend)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        const int64_t start = by_idx ? objs[mid].idx0 : objs[mid].wg0;
+        if (start <= w)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return __builtin_amdgcn_readfirstlane(lo);
+}
+
+// XCD-aware global work index (as decode_block): XCD b & 7 gets a contiguous range of the launch's work items
+__device__ __forceinline__ int64_t xcd_work_index(int64_t total) {
+    const int64_t b = blockIdx.x;
+    if ((total & 7) == 0) return (b & 7) * (total >> 3) + (b >> 3);
+    return b;
+}
+
+__device__ __forceinline__ MatmulParams ragged_params(const RaggedObj &d) {
+    MatmulParams q{};
+    q.in = d.in + d.col0;
+    q.coef = d.coef;
+    q.out = d.out + d.col0;
+    q.hdr = d.hdr;
+    q.in_row = d.in_row;
+    q.coef_row = d.coef_row;
+    q.out_row = d.out_row;
+    q.hdr_row = d.hdr_row;
+    q.n_out = d.n_out;
+    q.n_in = d.n_in;
+    q.width = d.width;
+    q.n_obj = 1;
+    return q;
+}
+
+// the block-address stream of every object of the table (all wave classes at once): entry e of object o is the
+// absolute address of the code block of coefficient c = coef[row][j] (0 past n_out), laid out [rt][j][row in tile]
+// from objs[o].idx0, as bsj_offset_kernel lays out one object
+__global__ __launch_bounds__(256) void ragged_offset_kernel(const RaggedObj *objs, int n, int64_t entries,
+                                                            uint64_t *stream, uint64_t base) {
+    const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (e >= entries) return;
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (objs[mid].idx0 <= e)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    const RaggedObj &d = objs[lo];
+    const int64_t l = e - d.idx0;
+    const int tr = d.tile_rows;
+    const int i = int(l % tr);
+    const int j = int((l / tr) % d.n_in);
+    const int rt = int(l / (int64_t(tr) * d.n_in));
+    const int row = rt * tr + i;
+    const uint32_t c = row < d.n_out ? d.coef[int64_t(row) * d.coef_row + j] : 0u;
+#ifdef RLNC_BSJ_SOFFSETS
+    stream[e] = base + kBsjSharedOff[c];
+#else
+    stream[e] = base + uint64_t(c) * RLNC_BSJ_BLOCK_BYTES;
+#endif
+}
+
+template <int W>
+__global__ __launch_bounds__(64 * W) void gf_matmul_bsj_ragged_kernel(const RaggedObj *objs, int n, int64_t total,
+                                                                      const uint64_t *stream) {
+    const int64_t w = xcd_work_index(total);
+    const int o = ragged_find(objs, n, w, false);
+    const RaggedObj &d = objs[o];
+    const int64_t l = w - d.wg0;
+    const int rt = int(l % d.row_tiles), cb = int(l / d.row_tiles);
+    const MatmulParams q = ragged_params(d);
+    bsj_tile<W, true, false>(q, stream + d.idx0, d.row_tiles, rt, cb, 0, 1u, nullptr);
+}
+
+// tails and shapes the bit-sliced program does not take: the perm kernel's tile on one object (byte-granular
+// loads, vector ones for full slots of an aligned object)
+template <bool AL>
+__device__ __forceinline__ void perm_ragged_tile(const MatmulParams &q, int rt, int cb) {
+    constexpr int NT = kRaggedPermRows;
+    __shared__ uint4 s_t01[kKC][NT];
+    __shared__ uint32_t s_t2[kKC][NT];
+    Tile t;
+    t.obj = 0;
+    t.cb = cb;
+    t.row0 = rt * NT;
+    t.rows_here = min(NT, q.n_out - t.row0);
+    t.col = int64_t(cb) * kColBlock + int64_t(threadIdx.x) * kBytesPerThread;
+    t.nbytes = t.col < q.width ? int(min<int64_t>(kBytesPerThread, q.width - t.col)) : 0;
+    const uint8_t *in_base = q.in + t.col;
+    const uint8_t *coef_base = q.coef + int64_t(t.row0) * q.coef_row;
+    uint32_t acc[NT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0u;
+    for (int j0 = 0; j0 < q.n_in; j0 += kKC) {
+        const int kc = min(kKC, q.n_in - j0);
+        if (j0) __syncthreads();
+        for (int e = threadIdx.x; e < kKC * NT; e += kThreads) {
+            const int i = e % NT, j = e / NT;
+            const uint8_t c = (i < t.rows_here && j < kc) ? coef_base[int64_t(i) * q.coef_row + j0 + j] : uint8_t(0);
+            const PermTable pt = make_perm_table(c);
+            s_t01[j][i] = make_uint4(pt.t0lo, pt.t0hi, pt.t1lo, pt.t1hi);
+            s_t2[j][i] = pt.t2;
+        }
+        __syncthreads();
+        if (t.nbytes > 0) {
+            const uint8_t *rowp = in_base + int64_t(j0) * q.in_row;
+            for (int j = 0; j < kc; ++j) {
+                const uint4 x = load16<AL>(rowp + int64_t(j) * q.in_row, t.nbytes);
+                const Sel a = selectors(x);
+#pragma unroll
+                for (int i = 0; i < NT; ++i) {
+                    const uint4 ta = s_t01[j][i];
+                    const uint32_t ta2 = s_t2[j][i];
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq)
+                        acc[i][qq] = xor3(xor3(acc[i][qq], vperm(ta.y, ta.x, a.s0[qq]), vperm(ta.w, ta.z, a.s1[qq])),
+                                          vperm(ta2, ta2, a.s2[qq]), 0u);
+                }
+            }
+        }
+    }
+    if (t.nbytes > 0) {
+        uint8_t *out_base = q.out + int64_t(t.row0) * q.out_row + t.col;
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+            if (i < t.rows_here)
+                store16<AL>(out_base + int64_t(i) * q.out_row, make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]),
+                            t.nbytes);
+    }
+    copy_header(q, t);
+}
+
+__global__ __launch_bounds__(kThreads) void gf_matmul_perm_ragged_kernel(const RaggedObj *objs, int n, int64_t total) {
+    const int64_t w = xcd_work_index(total);
+    const int o = ragged_find(objs, n, w, false);
+    const RaggedObj &d = objs[o];
+    const int64_t l = w - d.wg0;
+    const int rt = int(l % d.row_tiles), cb = int(l / d.row_tiles);
+    const MatmulParams q = ragged_params(d);
+    if (d.aligned)
+        perm_ragged_tile<true>(q, rt, cb);
+    else
+        perm_ragged_tile<false>(q, rt, cb);
 }
 
 // strided row copy (the coded pieces' coefficient headers, encoder.rs:246-248): one byte per thread
@@ -1448,7 +1633,11 @@ size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v) {
          v != MatmulVariant::BitSlicedJumpShared8 && v != MatmulVariant::BitSlicedJumpRun) ||
         p.n_out <= 0 || p.n_in <= 0 || p.n_obj <= 0)
         return 0;
+#ifdef RLNC_AB_VARIANTS
     if (v == MatmulVariant::BitSliced) return bs_eligible(p, matmul_aligned(p)) ? bs_scratch_bytes(p) : 0;
+#else
+    if (v == MatmulVariant::BitSliced) return 0;
+#endif
     return bsj_eligible(p, matmul_aligned(p))
                ? bsj_scratch_bytes(p, v == MatmulVariant::BitSlicedJumpShared8 || v == MatmulVariant::BitSlicedJumpRun)
                : 0;
@@ -1473,15 +1662,28 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
         t.hdr = nullptr;
         return launch_matmul(t, s, MatmulVariant::Perm);
     }
+#ifndef RLNC_AB_VARIANTS
+    if (v != MatmulVariant::Perm && v != MatmulVariant::NibbleLds && v != MatmulVariant::BitSlicedJump &&
+        v != MatmulVariant::BitSlicedJumpShared && v != MatmulVariant::BitSlicedJumpShared8)
+        return hipErrorInvalidValue;  // the A/B variants exist in diagnostic builds only
+#endif
     if (v == MatmulVariant::BitSliced || jump) {
         const bool run = v == MatmulVariant::BitSlicedJumpRun;
         const bool share = v == MatmulVariant::BitSlicedJumpShared || v == MatmulVariant::BitSlicedJumpShared8 || run;
         const bool wide = v == MatmulVariant::BitSlicedJumpShared8 || run;
         v = MatmulVariant::Perm;  // whatever the bit-sliced kernels do not cover
+#ifdef RLNC_AB_VARIANTS
         if (jump ? bsj_eligible(p, aligned) : bs_eligible(p, aligned)) {
+#else
+        if (bsj_eligible(p, aligned)) {
+#endif
             int64_t full = 0;
+#ifdef RLNC_AB_VARIANTS
             hipError_t e = jump ? launch_bsj(p, s, scratch, scratch_bytes, full, share, wide, run)
                                 : launch_bs(p, s, scratch, scratch_bytes, full);
+#else
+            hipError_t e = launch_bsj(p, s, scratch, scratch_bytes, full, share, wide, run);
+#endif
             if (e != hipSuccess || full == p.width) return e;
             MatmulParams t = p;
             t.in = p.in + full;
@@ -1491,6 +1693,7 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
             return launch_matmul(t, s, v);
         }
     }
+#ifdef RLNC_AB_VARIANTS
     if (aligned && (v == MatmulVariant::Wide || v == MatmulVariant::Wide4)) {
         if (v == MatmulVariant::Wide4) return p.n_out <= 4 ? launch_wide_split<4, 4>(p, s) : launch_wide_split<8, 4>(p, s);
         if (p.n_out <= 4) return launch_wide_split<4, 2>(p, s);
@@ -1498,6 +1701,7 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
         return launch_wide_split<16, 2>(p, s);
     }
     if (v == MatmulVariant::Wide || v == MatmulVariant::Wide4) v = MatmulVariant::Perm;
+#endif
     // narrow (< one 4 KiB column block, e.g. the ragged tail of a recode over k + L bytes): the work is the
     // sources x rows chain of one block, so split the rows over many workgroups (2 rows each)
     if (p.width < kColBlock && p.n_out > 2) {
@@ -1511,6 +1715,47 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
     if (p.n_out <= 8) return launch_nt<8>(p, s, v, aligned);
     if (p.n_out <= 16) return launch_nt<16>(p, s, v, aligned);
     return launch_nt<32>(p, s, v, aligned);
+}
+
+bool ragged_bsj_eligible(const uint8_t *in, const uint8_t *out, int64_t in_row, int64_t out_row, int64_t width,
+                         int n_out) {
+    return al16(in) && al16(out) && al16(in_row) && al16(out_row) && width >= kBsjColBlock && n_out >= 4 &&
+           in_row < (int64_t(1) << 32) && out_row < (int64_t(1) << 32);
+}
+
+int ragged_bsj_waves(int n_out) { return n_out > 32 ? 8 : 4; }
+
+hipError_t ragged_bsj_base(hipStream_t s, void *probe_scratch, uint64_t &base) {
+    return bsj_shared_base(s, probe_scratch, base);
+}
+
+hipError_t launch_ragged_offsets(const RaggedObj *objs, int n, int64_t entries, void *stream, uint64_t base,
+                                 hipStream_t s) {
+    if (entries <= 0) return hipSuccess;
+    if ((entries + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ragged_offset_kernel, dim3(unsigned((entries + 255) / 256)), dim3(256), 0, s, objs, n, entries,
+                       static_cast<uint64_t *>(stream), base);
+    return hipGetLastError();
+}
+
+hipError_t launch_ragged_bsj(int W, const RaggedObj *objs, int n, int64_t wgs, const void *stream, hipStream_t s) {
+    if (wgs <= 0) return hipSuccess;
+    if (wgs > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    const uint64_t *st = static_cast<const uint64_t *>(stream);
+    if (W == 8)
+        hipLaunchKernelGGL(gf_matmul_bsj_ragged_kernel<8>, dim3(unsigned(wgs)), dim3(512), 0, s, objs, n, wgs, st);
+    else if (W == 4)
+        hipLaunchKernelGGL(gf_matmul_bsj_ragged_kernel<4>, dim3(unsigned(wgs)), dim3(256), 0, s, objs, n, wgs, st);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_ragged_perm(const RaggedObj *objs, int n, int64_t wgs, hipStream_t s) {
+    if (wgs <= 0) return hipSuccess;
+    if (wgs > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gf_matmul_perm_ragged_kernel, dim3(unsigned(wgs)), dim3(kThreads), 0, s, objs, n, wgs);
+    return hipGetLastError();
 }
 
 hipError_t launch_mul_vec_by_scalar(uint8_t *vec, int64_t len, uint8_t scalar, hipStream_t s) {

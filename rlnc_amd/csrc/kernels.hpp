@@ -51,6 +51,38 @@ size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v);
 hipError_t launch_matmul(const MatmulParams &p, hipStream_t stream, MatmulVariant v = MatmulVariant::Perm,
                          void *scratch = nullptr, size_t scratch_bytes = 0);
 
+// ---- ragged batches: one launch per kernel stage over objects of different shapes (wire.hip) -----------------
+// One object's part of a ragged matmul launch (device-side descriptor table, 120 bytes).  Objects are ordered by
+// wg0 (and, in the block-address stream, by idx0).
+struct RaggedObj {
+    const uint8_t *in;    // source rows (n_in of them), row stride in_row
+    const uint8_t *coef;  // n_out x n_in coefficients, row stride coef_row
+    uint8_t *out;         // n_out output rows, row stride out_row
+    uint8_t *hdr;         // coefficient rows copied here too (coded-piece header), or nullptr
+    int64_t in_row, coef_row, out_row, hdr_row;
+    int64_t col0;   // first column (bytes) of this launch's part of the object
+    int64_t width;  // columns of this part, from col0
+    int64_t wg0;    // the object's first workgroup in its launch
+    int64_t idx0;   // the object's first entry in the block-address stream (bit-sliced part)
+    int32_t n_out, n_in;
+    int32_t row_tiles, col_blocks;
+    int32_t tile_rows;  // bit-sliced part: 8 x waves per workgroup
+    int32_t aligned;    // perm part: operands 16-byte aligned (vector loads for full slots)
+};
+static_assert(sizeof(RaggedObj) == 120, "RaggedObj layout");
+constexpr int kRaggedPermRows = 8;     // output rows per workgroup of the ragged perm kernel
+constexpr int kRaggedColBlock = 4096;  // columns per workgroup (both ragged kernels)
+// the bit-sliced program takes whole 4 KiB column blocks of 16-byte-aligned operands with >= 4 output rows
+bool ragged_bsj_eligible(const uint8_t *in, const uint8_t *out, int64_t in_row, int64_t out_row, int64_t width,
+                         int n_out);
+int ragged_bsj_waves(int n_out);  // 4 (32-row tiles) up to 32 output rows, else 8 (64-row tiles)
+// the shared program's block table address (probe_scratch: >= 8 device bytes; synchronous the first time)
+hipError_t ragged_bsj_base(hipStream_t s, void *probe_scratch, uint64_t &base);
+hipError_t launch_ragged_offsets(const RaggedObj *objs, int n, int64_t entries, void *stream, uint64_t base,
+                                 hipStream_t s);
+hipError_t launch_ragged_bsj(int W, const RaggedObj *objs, int n, int64_t wgs, const void *stream, hipStream_t s);
+hipError_t launch_ragged_perm(const RaggedObj *objs, int n, int64_t wgs, hipStream_t s);
+
 // Element-wise primitives (src/common/simd/mod.rs:18-119) on one device vector.
 hipError_t launch_mul_vec_by_scalar(uint8_t *vec, int64_t len, uint8_t scalar, hipStream_t s);
 hipError_t launch_add_vectors(uint8_t *dst, const uint8_t *src, int64_t len, hipStream_t s);
@@ -79,9 +111,26 @@ struct RrefParams {
     int32_t *rank;
     int lds_only;  // clean-state path (A/B, all exact): 0 auto (blocked clean run when k + m <= 256, else 4);
                    // 1 LDS; 2 registers, one wave; 3 blocked clean run (gf_rref_block_kernel); 4 registers, multi-wave
+    const struct RrefObj *objs = nullptr;  // ragged batch: object o's shape and buffers (the fields above unused)
 };
+// One object of a ragged elimination launch (rlnc_decode_ragged): T is k x m row-major, status m entries.
+struct RrefObj {
+    const uint8_t *pieces;
+    int64_t piece_stride;
+    uint8_t *T;
+    int32_t *status;
+    int32_t *rank;
+    int32_t k, m;
+};
+// ragged elimination: one workgroup per object of the device table objs (n objects, k + m <= 256 each when
+// block = true -- the blocked clean run -- else the one-wave LDS kernel); lds = the largest object's need
+size_t rref_block_lds_bytes_public(int k, int m);
+hipError_t launch_rref_ragged(const RrefObj *objs, int n, bool block, size_t lds, int hdr_lds, hipStream_t s);
+size_t rref_lds_bytes_staged_public(int k, int m);
 constexpr size_t kRrefMaxLds = 160 * 1024;
 size_t rref_lds_bytes(int k, int m);
+// the blocked clean-run kernel (decode path 5, and what 0 / 2 pick) applies: a row fits one wave (k + m <= 256)
+bool rref_block_eligible(int k, int m);
 hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s);
 
 // final_len with the decoder's rank: objects with rank < k report NotAllPiecesReceivedYet

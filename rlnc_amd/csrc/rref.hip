@@ -688,13 +688,30 @@ __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, u
 // G > 0: the clean state runs on registers (reg_run<G, RT>); G = 0: on LDS (clean_append).  NW > 1: the
 // initial clean run is spread over NW waves (reg_run_mw); then waves 1..NW-1 end and wave 0 continues alone
 // (S_BARRIER waits only for the waves that have not terminated).
+// ragged batch (p.objs): this workgroup's object replaces the uniform fields, as object 0 of a one-object batch
+__device__ __forceinline__ void rref_ragged_object(RrefParams &p, int &o) {
+    if (p.objs == nullptr) return;
+    const RrefObj &d = p.objs[o];
+    p.pieces = d.pieces;
+    p.obj_stride = 0;
+    p.piece_stride = d.piece_stride;
+    p.k = __builtin_amdgcn_readfirstlane(d.k);
+    p.m = __builtin_amdgcn_readfirstlane(d.m);
+    p.T = d.T;
+    p.T_obj = 0;
+    p.status = d.status;
+    p.rank = d.rank;
+    o = 0;
+}
+
 template <int G, int RT, int NW, int MG = 4, int MRTW = 2>
 __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, int hdr_lds) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;  // kTabEntries × kTabDw dwords
     const int lane = threadIdx.x;  // the single-wave code below runs in wave 0 only (lane < 64)
     const int tid = threadIdx.x;
-    const int o = blockIdx.x;
+    int o = blockIdx.x;
+    rref_ragged_object(p, o);
     const int k = p.k, m = p.m;
 #ifdef RLNC_RREF_PROFILE  // diagnostic build: statuses become per-piece cycle counts, rank the setup cycles
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
@@ -961,7 +978,8 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int o = blockIdx.x;
+    int o = blockIdx.x;
+    rref_ragged_object(p, o);
     const int k = p.k, m = p.m;
     const int kH = (k + 3) & ~3;  // staged header stride (dword-aligned coefficient groups, zero padded)
     Mat M;
@@ -1355,12 +1373,51 @@ size_t rref_block_lds_bytes(int k, int m) {
 
 }  // namespace
 
+bool rref_block_eligible(int k, int m) {
+    return rref_row_dwords(k, m) <= 64 && rref_block_lds_bytes(k, m) <= kRrefMaxLds;
+}
+
 size_t rref_lds_bytes(int k, int m) {
     return kTabEntries * kTabDw * 4 + size_t(k + 1) * 4 * size_t(rref_row_dwords(k, m)) + 4 * ((size_t(m) + 3) & ~size_t(3));
 }
 // + the staged headers, + 2 × 4 × 64 dwords of multi-wave partial sums
 static size_t rref_lds_bytes_staged(int k, int m) {
     return rref_lds_bytes(k, m) + ((size_t(k) * m + 15) & ~size_t(15)) + 2 * 4 * 64 * 4;
+}
+
+size_t rref_block_lds_bytes_public(int k, int m) { return rref_block_lds_bytes(k, m); }
+size_t rref_lds_bytes_staged_public(int k, int m) { return rref_lds_bytes_staged(k, m); }
+
+hipError_t launch_rref_ragged(const RrefObj *objs, int n, bool block, size_t lds, int hdr_lds, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (lds > kRrefMaxLds) return hipErrorInvalidValue;
+    RrefParams p{};
+    p.objs = objs;
+    p.n_obj = n;
+    // the dynamic-LDS attribute of both kernels (a first launch through launch_rref_batch may not have run yet)
+    static std::mutex mu;
+    static bool attr_set[64] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        if (!attr_set[dev]) {
+            e = hipFuncSetAttribute(reinterpret_cast<const void *>(&gf_rref_block_kernel<kBlkNW, 8>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, int(kRrefMaxLds));
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute(reinterpret_cast<const void *>(&gf_rref_batch_kernel<0, 1, 1>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, int(kRrefMaxLds));
+            if (e != hipSuccess) return e;
+            attr_set[dev] = true;
+        }
+    }
+    if (block)
+        hipLaunchKernelGGL((gf_rref_block_kernel<kBlkNW, 8>), dim3(n), dim3(64 * kBlkNW), lds, s, p);
+    else
+        hipLaunchKernelGGL((gf_rref_batch_kernel<0, 1, 1>), dim3(n), dim3(64), lds, s, p, hdr_lds);
+    return hipGetLastError();
 }
 
 hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
@@ -1374,7 +1431,7 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     // the blocked clean run (4 waves per object, the default) when the row fits one wave (k + m <= 256)
     if (!small_many && (p.lds_only == 0 || p.lds_only == 3) && rref_row_dwords(p.k, p.m) <= 64 &&
         rref_block_lds_bytes(p.k, p.m) <= kRrefMaxLds) {
-        // A/B knob (read once): RLNC_BLK = 8 or 16 pieces per block (NW = 4 waves)
+#ifdef RLNC_AB_VARIANTS
         // A/B knob (read once): RLNC_BLK = 8 or 16 pieces per block (profiles/r02_elim_ab.txt)
         static const int blk = [] {
             const char *e = getenv("RLNC_BLK");
@@ -1382,6 +1439,10 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
             return v == 8 || v == 16 ? v : kBlkDefault;
         }();
         auto kern = blk == 16 ? &gf_rref_block_kernel<kBlkNW, 16> : &gf_rref_block_kernel<kBlkNW, 8>;
+#else
+        static_assert(kBlkDefault == 8, "the shipped block size");
+        auto kern = &gf_rref_block_kernel<kBlkNW, 8>;
+#endif
         static std::mutex mu;
         static bool attr_set[64] = {};
         int dev = 0;
@@ -1391,7 +1452,11 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
         {
             std::lock_guard<std::mutex> lock(mu);
             if (!attr_set[dev]) {
+#ifdef RLNC_AB_VARIANTS
                 for (auto f : {&gf_rref_block_kernel<kBlkNW, 8>, &gf_rref_block_kernel<kBlkNW, 16>}) {
+#else
+                for (auto f : {&gf_rref_block_kernel<kBlkNW, 8>}) {
+#endif
                     e = hipFuncSetAttribute(reinterpret_cast<const void *>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
                                             int(kRrefMaxLds));
                     if (e != hipSuccess) return e;
@@ -1411,6 +1476,7 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     const int D = rref_row_dwords(p.k, p.m);
     auto kern = &gf_rref_batch_kernel<0, 1, 1>;
     int threads = 64;
+#ifdef RLNC_AB_VARIANTS
     if (p.lds_only != 1 && hdr_lds) {  // the register paths read the staged headers
         const bool mw = (p.lds_only == 0 && !small_many) || p.lds_only == 4;
         if (D <= 16 && p.k <= 32) {
@@ -1420,6 +1486,12 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
         }  // k = 128 (<0, 1, 4, 1, 32>: 3.8 ms for 512 objects) stays on the one-wave LDS path (2.5 ms)
         if (mw && kern != &gf_rref_batch_kernel<0, 1, 1>) threads = 256;
     }
+#else
+    // shipped paths: the blocked run above (k + m <= 256), the one-wave register kernel for many small objects,
+    // else the one-wave LDS kernel (the multi-wave register forms of decode paths 3/4/6 are diagnostic builds only)
+    if (p.lds_only != 0 || (small_many && !hdr_lds)) return hipErrorInvalidValue;
+    if (small_many && D <= 16 && p.k <= 32) kern = &gf_rref_batch_kernel<4, 8, 1>;
+#endif
     // the 160 KiB dynamic-LDS attribute, once per device (function attributes are per device), under a lock
     {
         static std::mutex mu;
@@ -1430,9 +1502,13 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
         if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
         std::lock_guard<std::mutex> lock(mu);
         if (!attr_set[dev]) {
+#ifdef RLNC_AB_VARIANTS
             for (auto f : {&gf_rref_batch_kernel<0, 1, 1>, &gf_rref_batch_kernel<4, 8, 1>,
                            &gf_rref_batch_kernel<4, 8, 4, 4, 2>, &gf_rref_batch_kernel<2, 32, 1>,
                            &gf_rref_batch_kernel<2, 32, 4, 2, 8>}) {
+#else
+            for (auto f : {&gf_rref_batch_kernel<0, 1, 1>, &gf_rref_batch_kernel<4, 8, 1>}) {
+#endif
                 e = hipFuncSetAttribute(reinterpret_cast<const void *>(f),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(kRrefMaxLds));
                 if (e != hipSuccess) return e;

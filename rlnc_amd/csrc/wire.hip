@@ -1,20 +1,93 @@
 // wire.hip — the data formats either side of the hot path, on the device:
 //   * Encoder::new's padded image (encoder.rs:85-106, marker consts.rs:5) written by a kernel from a byte string
 //     already in HBM: rlnc_pad_device / rlnc_pad_batch_device / rlnc_encoder_new_device;
-//   * a ragged batch: objects with their own k, L, n and buffers in one call (rlnc_encode_ragged), as socket or
-//     file ingestion produces them.
+//   * ragged batches: objects with their own shapes and buffers in one call -- the sender's encode
+//     (rlnc_encode_ragged) and the receiver's recode and decode (rlnc_recode_ragged, rlnc_decode_ragged), as
+//     socket or file ingestion produces them.  Each kernel stage is ONE launch over a device-side descriptor table
+//     (per wave class of the bit-sliced program), not one launch per object or per shape.
 // The coeffs ‖ data framing of a coded piece is written by the matmul kernels themselves (header copy), and the
-// decoder's marker scan by last_nonzero_kernel (kernels.hip).
-#include <map>
-#include <tuple>
+// decoder's marker scan by a kernel here / in kernels.hip.
+#include <algorithm>
 
 #include "context.hpp"
+#include "elimination.hpp"
 #include "gf256.hpp"
 
 using namespace rlnc::eng;
 
 namespace {
 
+// ---------------------------------------------------------------------------------------------------------------
+// Descriptor tables on the device.
+//   eager: pinned staging (guarded by an event: the previous upload's copy must have run before the staging buffer
+//          is rewritten) → the context's table workspace, one copy on the context stream;
+//   inside a HIP stream capture: a region of a capture arena that is never handed out again, filled by kernels
+//          that carry the bytes as kernel arguments, so every replay of the graph rewrites exactly the captured
+//          table -- a later eager call (which uses the staging path) cannot change what a replay reads, and no host
+//          synchronisation on an event recorded inside the capture is needed.  The arena is reserved by eager calls
+//          (allocation inside a capture is not allowed): run a call once eagerly before capturing it, as for the
+//          workspaces (include/rlnc_hip.h, "HIP graphs").
+// ---------------------------------------------------------------------------------------------------------------
+constexpr size_t kChunk = 3072;  // table bytes per fill kernel (kernel arguments stay well below 4 KiB)
+struct TableChunk {
+    uint32_t bytes;
+    uint32_t pad;
+    uint8_t data[kChunk];
+};
+
+__global__ __launch_bounds__(256) void table_fill_kernel(uint8_t *dst, TableChunk c) {
+    for (uint32_t i = threadIdx.x; i < c.bytes; i += 256) dst[i] = c.data[i];
+}
+
+int upload_table(rlnc_context *ctx, const void *host, size_t bytes, void **dev) {
+    const size_t need = round16(std::max<size_t>(bytes, 16));
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(ctx->stream, &cs));
+    if (cs != hipStreamCaptureStatusNone) {
+        auto &arenas = ctx->cap_arenas;
+        if (arenas.empty() || ctx->cap_used + need > arenas.back()->cap)
+            return set_error(RLNC_ERR_INVALID_ARGUMENT,
+                             "descriptor table of %zu bytes inside a HIP graph capture: run the same call once "
+                             "eagerly before capturing it (that reserves the capture arena)",
+                             bytes);
+        uint8_t *d = arenas.back()->as<uint8_t>() + ctx->cap_used;
+        ctx->cap_used += need;
+        for (size_t off = 0; off < bytes; off += kChunk) {
+            TableChunk c{};
+            c.bytes = uint32_t(std::min(kChunk, bytes - off));
+            std::memcpy(c.data, static_cast<const uint8_t *>(host) + off, c.bytes);
+            hipLaunchKernelGGL(table_fill_kernel, dim3(1), dim3(256), 0, ctx->stream, d + off, c);
+            HIP_TRY(hipGetLastError());
+        }
+        *dev = d;
+        return RLNC_OK;
+    }
+    // eager: keep room in the capture arena for a captured call of this size (never moved once handed out)
+    {
+        auto &arenas = ctx->cap_arenas;
+        const size_t reserve = 2 * need + (size_t(64) << 10);
+        if (!ctx->graph_bound && (arenas.empty() || ctx->cap_used + reserve > arenas.back()->cap)) {
+            std::unique_ptr<DevBuf> a(new (std::nothrow) DevBuf);
+            if (!a) return set_error(RLNC_ERR_OUT_OF_MEMORY, "capture arena");
+            if (int st = a->ensure(std::max<size_t>(size_t(1) << 20, 4 * reserve))) return st;
+            arenas.push_back(std::move(a));
+            ctx->cap_used = 0;
+        }
+    }
+    int st;
+    if (ctx->tab_ev) HIP_TRY(hipEventSynchronize(ctx->tab_ev));
+    if ((st = ctx->grow(ctx->pin_tab, need)) || (st = ctx->grow(ctx->ws_tab, need))) return st;
+    std::memcpy(ctx->pin_tab.p, host, bytes);
+    HIP_TRY(hipMemcpyAsync(ctx->ws_tab.p, ctx->pin_tab.p, bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (!ctx->tab_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->tab_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ctx->tab_ev, ctx->stream));
+    *dev = ctx->ws_tab.p;
+    return RLNC_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Encoder::new's padded image
+// ---------------------------------------------------------------------------------------------------------------
 struct PadDesc {
     const uint8_t *data;
     uint8_t *out;
@@ -48,27 +121,13 @@ __global__ __launch_bounds__(256) void pad_kernel(const PadDesc *descs) {
     }
 }
 
-// descriptor upload: pinned staging guarded by an event (the previous call's copy must have run before the
-// staging buffer is rewritten), device copy in the context's workspace
-int upload_descs(rlnc_context *ctx, const void *host, size_t bytes, void **dev) {
-    int st;
-    if (ctx->tab_ev) HIP_TRY(hipEventSynchronize(ctx->tab_ev));
-    if ((st = ctx->grow(ctx->pin_tab, bytes)) || (st = ctx->grow(ctx->ws_tab, bytes))) return st;
-    std::memcpy(ctx->pin_tab.p, host, bytes);
-    HIP_TRY(hipMemcpyAsync(ctx->ws_tab.p, ctx->pin_tab.p, bytes, hipMemcpyHostToDevice, ctx->stream));
-    if (!ctx->tab_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->tab_ev, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(ctx->tab_ev, ctx->stream));
-    *dev = ctx->ws_tab.p;
-    return RLNC_OK;
-}
-
 int launch_pad(rlnc_context *ctx, const std::vector<PadDesc> &d) {
     int64_t max_blocks = 0;
     for (const auto &x : d) max_blocks = std::max<int64_t>(max_blocks, ((x.L + 15) / 16 * x.k + 255) / 256);
     if (max_blocks == 0) return RLNC_OK;
     if (max_blocks > 0x7FFFFFFF || d.size() > 65535) return set_error(RLNC_ERR_INVALID_ARGUMENT, "pad batch too large");
     void *dd = nullptr;
-    int st = upload_descs(ctx, d.data(), d.size() * sizeof(PadDesc), &dd);
+    int st = upload_table(ctx, d.data(), d.size() * sizeof(PadDesc), &dd);
     if (st) return st;
     hipLaunchKernelGGL(pad_kernel, dim3(unsigned(max_blocks), unsigned(d.size())), dim3(256), 0, ctx->stream,
                        static_cast<const PadDesc *>(dd));
@@ -87,7 +146,158 @@ int pad_check(const rlnc_pad_desc &d, PadDesc &o) {
     return RLNC_OK;
 }
 
-int64_t addr(const void *p) { return int64_t(reinterpret_cast<intptr_t>(p)); }
+// ---------------------------------------------------------------------------------------------------------------
+// Ragged matmul: Out_o = Coef_o ⊗ In_o for objects of any shapes, one launch per kernel stage.  Each object's whole
+// 4 KiB column blocks go to the bit-sliced program (the hot path of the uniform batches, §4.1 of DESIGN.md) -- one
+// launch for objects of <= 32 output rows (4-wave, 32-row tiles) and one for larger ones (8-wave, 64-row tiles), after
+// ONE launch that writes every object's block-address stream -- and whatever it does not take (the ragged < 4 KiB
+// tail, unaligned operands, < 4 output rows) to one launch of the perm kernel.  So at most 4 launches, whatever the
+// number of objects and shapes.
+// ---------------------------------------------------------------------------------------------------------------
+struct MatmulJob {
+    const uint8_t *in, *coef;
+    uint8_t *out, *hdr;
+    int64_t in_row, coef_row, out_row, hdr_row, width;
+    int n_out, n_in;
+};
+
+bool al16p(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int ragged_matmul(rlnc_context *ctx, const std::vector<MatmulJob> &jobs) {
+    using rlnc::RaggedObj;
+    std::vector<RaggedObj> w4, w8, perm;
+    // the bit-sliced program needs its block table's address (one probe per device, synchronous the first time;
+    // inside a capture that first probe cannot run: everything then takes the perm kernel, bit-identical)
+    uint64_t base = 0;
+    bool any_bsj = false;
+    for (const auto &j : jobs)
+        any_bsj |= j.n_out > 0 && j.n_in > 0 && j.width > 0 &&
+                   rlnc::ragged_bsj_eligible(j.in, j.out, j.in_row, j.out_row, j.width, j.n_out);
+    int st;
+    if (any_bsj) {
+        if ((st = ctx->grow(ctx->ws_idx, 512))) return st;
+        HIP_TRY(rlnc::ragged_bsj_base(ctx->stream, ctx->ws_idx.p, base));
+    }
+    for (const auto &j : jobs) {
+        if (j.n_out <= 0 || j.n_in <= 0 || j.width <= 0) continue;
+        int64_t full = 0;
+        if (base != 0 && rlnc::ragged_bsj_eligible(j.in, j.out, j.in_row, j.out_row, j.width, j.n_out)) {
+            full = (j.width / rlnc::kRaggedColBlock) * rlnc::kRaggedColBlock;
+            const int W = rlnc::ragged_bsj_waves(j.n_out);
+            RaggedObj d{};
+            d.in = j.in;
+            d.coef = j.coef;
+            d.out = j.out;
+            d.hdr = j.hdr;
+            d.in_row = j.in_row;
+            d.coef_row = j.coef_row;
+            d.out_row = j.out_row;
+            d.hdr_row = j.hdr_row;
+            d.col0 = 0;
+            d.width = full;
+            d.n_out = j.n_out;
+            d.n_in = j.n_in;
+            d.tile_rows = 8 * W;
+            d.row_tiles = (j.n_out + d.tile_rows - 1) / d.tile_rows;
+            d.col_blocks = int(full / rlnc::kRaggedColBlock);
+            (W == 8 ? w8 : w4).push_back(d);
+        }
+        if (full < j.width) {
+            RaggedObj d{};
+            d.in = j.in;
+            d.coef = j.coef;
+            d.out = j.out;
+            d.hdr = full ? nullptr : j.hdr;  // the bit-sliced part (column block 0) already wrote the header
+            d.in_row = j.in_row;
+            d.coef_row = j.coef_row;
+            d.out_row = j.out_row;
+            d.hdr_row = j.hdr_row;
+            d.col0 = full;
+            d.width = j.width - full;
+            d.n_out = j.n_out;
+            d.n_in = j.n_in;
+            d.row_tiles = (j.n_out + rlnc::kRaggedPermRows - 1) / rlnc::kRaggedPermRows;
+            d.col_blocks = int((d.width + rlnc::kRaggedColBlock - 1) / rlnc::kRaggedColBlock);
+            d.aligned = al16p(j.in + full) && al16p(j.out + full) && (j.in_row & 15) == 0 && (j.out_row & 15) == 0;
+            perm.push_back(d);
+        }
+    }
+    const size_t n4 = w4.size(), n8 = w8.size(), np = perm.size();
+    if (n4 + n8 + np == 0) return RLNC_OK;
+    if (n4 + n8 + np > 0x7FFFFFFF) return set_error(RLNC_ERR_INVALID_ARGUMENT, "ragged batch too large");
+    // table: [4-wave bit-sliced][8-wave bit-sliced][perm]; wg0 numbered per launch, idx0 across both bit-sliced ones
+    std::vector<RaggedObj> tab;
+    tab.reserve(n4 + n8 + np);
+    int64_t idx = 0, wg4 = 0, wg8 = 0, wgp = 0;
+    for (auto *v : {&w4, &w8})
+        for (auto &d : *v) {
+            int64_t &wg = v == &w4 ? wg4 : wg8;
+            d.wg0 = wg;
+            d.idx0 = idx;
+            wg += int64_t(d.row_tiles) * d.col_blocks;
+            idx += int64_t(d.row_tiles) * d.n_in * d.tile_rows;
+            tab.push_back(d);
+        }
+    for (auto &d : perm) {
+        d.wg0 = wgp;
+        wgp += int64_t(d.row_tiles) * d.col_blocks;
+        tab.push_back(d);
+    }
+    if (wg4 > 0x7FFFFFFF || wg8 > 0x7FFFFFFF || wgp > 0x7FFFFFFF)
+        return set_error(RLNC_ERR_INVALID_ARGUMENT, "ragged batch too large for one launch");
+    if (idx > 0 && (st = ctx->grow(ctx->ws_idx, size_t(idx) * 8 + 512))) return st;
+    void *dtab = nullptr;
+    if ((st = upload_table(ctx, tab.data(), tab.size() * sizeof(RaggedObj), &dtab))) return st;
+    const RaggedObj *t = static_cast<const RaggedObj *>(dtab);
+    HIP_TRY(rlnc::launch_ragged_offsets(t, int(n4 + n8), idx, ctx->ws_idx.p, base, ctx->stream));
+    HIP_TRY(rlnc::launch_ragged_bsj(4, t, int(n4), wg4, ctx->ws_idx.p, ctx->stream));
+    HIP_TRY(rlnc::launch_ragged_bsj(8, t + n4, int(n8), wg8, ctx->ws_idx.p, ctx->stream));
+    HIP_TRY(rlnc::launch_ragged_perm(t + n4 + n8, int(np), wgp, ctx->stream));
+    return RLNC_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Ragged get_decoded_data (decoder.rs:136-177): one wave per object scans its padded payload from the end (the last
+// nonzero byte must be the 0x81 marker, not at index 0), objects of rank < k report NotAllPiecesReceivedYet.
+// ---------------------------------------------------------------------------------------------------------------
+struct ScanObj {
+    const uint8_t *data;
+    const int32_t *rank;
+    int32_t *status;
+    int64_t *len_out;
+    int64_t len;
+    int32_t k, pad;
+};
+
+__global__ __launch_bounds__(64) void ragged_final_len_kernel(const ScanObj *objs) {
+    const ScanObj d = objs[blockIdx.x];
+    const int lane = threadIdx.x;
+    if (*d.rank < d.k) {  // decoder.rs:137-139
+        if (lane == 0) {
+            *d.status = RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;
+            *d.len_out = 0;
+        }
+        return;
+    }
+    int64_t last = -1;  // index of the last nonzero byte (wave-uniform after the reduction)
+    for (int64_t c = (d.len + 1023) / 1024 - 1; c >= 0 && last < 0; --c) {
+        int64_t mine = -1;
+        for (int q = 0; q < 16; ++q) {
+            const int64_t i = c * 1024 + int64_t(lane) * 16 + q;
+            if (i < d.len && d.data[i] != 0) mine = i;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const int64_t v = __shfl_xor(mine, o);
+            mine = v > mine ? v : mine;
+        }
+        last = mine;
+    }
+    if (lane == 0) {
+        const bool ok = last > 0 && d.data[last] == rlnc::kBoundaryMarker;
+        *d.status = ok ? RLNC_OK : RLNC_ERR_INVALID_DECODED_DATA_FORMAT;
+        *d.len_out = ok ? last : 0;
+    }
+}
 
 }  // namespace
 
@@ -113,10 +323,13 @@ int rlnc_pad_device(rlnc_context *ctx, const uint8_t *data_dev, size_t len, size
     return rlnc_pad_batch_device(ctx, &d, 1);
 }
 
+// encoder.rs:241-250 for every object: n coded pieces coeffs ‖ Σ coeffs·src each
 int rlnc_encode_ragged(rlnc_context *ctx, const rlnc_object_desc *objs, size_t count) {
     CHECK_ARG(ctx != nullptr);
     if (count == 0) return RLNC_OK;
     CHECK_ARG(objs != nullptr);
+    std::vector<MatmulJob> jobs;
+    jobs.reserve(count);
     for (size_t i = 0; i < count; ++i) {  // every descriptor is checked before anything is launched
         const rlnc_object_desc &o = objs[i];
         if (o.k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
@@ -125,63 +338,151 @@ int rlnc_encode_ragged(rlnc_context *ctx, const rlnc_object_desc *objs, size_t c
         CHECK_ARG(o.src && o.coeffs && o.pieces && o.n <= 0x7FFFFFFF && o.k <= 0x7FFFFFFF);
         CHECK_ARG(o.src_row_stride == 0 || o.src_row_stride >= o.L);
         CHECK_ARG(o.piece_row_stride == 0 || o.piece_row_stride >= o.k + o.L);
+        const int64_t ss = int64_t(o.src_row_stride ? o.src_row_stride : o.L);
+        const int64_t ps = int64_t(o.piece_row_stride ? o.piece_row_stride : o.k + o.L);
+        jobs.push_back(MatmulJob{o.src, o.coeffs, o.pieces + o.k, o.pieces, ss, int64_t(o.k), ps, ps, int64_t(o.L),
+                                 int(o.n), int(o.k)});
     }
     int st = ctx->activate();
     if (st || (st = ctx->note_capture())) return st;
-    // objects of one shape (k, L, n, strides) in input order; each maximal run whose buffers sit at one constant
-    // object stride is ONE launch (the kernels' object dimension), others one launch each
-    std::map<std::tuple<size_t, size_t, size_t, size_t, size_t>, std::vector<size_t>> groups;
+    return ragged_matmul(ctx, jobs);
+}
+
+// recoder.rs:122-153 for every object: out[i] = Σ_j r[i][j] · piece_j over the full pieces (coefficient header and
+// data are one linear map)
+int rlnc_recode_ragged(rlnc_context *ctx, const rlnc_recode_object_desc *objs, size_t count) {
+    CHECK_ARG(ctx != nullptr);
+    if (count == 0) return RLNC_OK;
+    CHECK_ARG(objs != nullptr);
+    std::vector<MatmulJob> jobs;
+    jobs.reserve(count);
     for (size_t i = 0; i < count; ++i) {
-        const rlnc_object_desc &o = objs[i];
-        if (o.n == 0) continue;
-        const size_t ss = o.src_row_stride ? o.src_row_stride : o.L;
-        const size_t ps = o.piece_row_stride ? o.piece_row_stride : o.k + o.L;
-        groups[{o.k, o.L, o.n, ss, ps}].push_back(i);
+        const rlnc_recode_object_desc &o = objs[i];
+        if (o.n == 0) return RLNC_ERR_NOT_ENOUGH_PIECES_TO_RECODE;  // recoder.rs:69-71
+        if (o.k + o.L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;       // :72-74
+        if (o.k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;              // :75-77
+        if (o.L == 0) return RLNC_ERR_PIECE_LENGTH_TOO_SHORT;        // :78-80 (full <= k)
+        if (o.n_recoded == 0) continue;
+        CHECK_ARG(o.pieces && o.r && o.out && o.n <= 0x7FFFFFFF && o.n_recoded <= 0x7FFFFFFF);
+        CHECK_ARG(o.piece_row_stride == 0 || o.piece_row_stride >= o.k + o.L);
+        CHECK_ARG(o.out_row_stride == 0 || o.out_row_stride >= o.k + o.L);
+        const int64_t ps = int64_t(o.piece_row_stride ? o.piece_row_stride : o.k + o.L);
+        const int64_t os = int64_t(o.out_row_stride ? o.out_row_stride : o.k + o.L);
+        jobs.push_back(MatmulJob{o.pieces, o.r, o.out, nullptr, ps, int64_t(o.n), os, 0, int64_t(o.k + o.L),
+                                 int(o.n_recoded), int(o.n)});
     }
-    for (auto &g : groups) {
-        const size_t k = std::get<0>(g.first), L = std::get<1>(g.first), n = std::get<2>(g.first);
-        const size_t ss = std::get<3>(g.first), ps = std::get<4>(g.first);
-        const auto &ix = g.second;
-        for (size_t a = 0; a < ix.size();) {
-            // extend the run while src / coeffs / pieces advance by the same strides as between the first two
-            size_t b = a + 1;
-            int64_t ds = 0, dc = 0, dp = 0;
-            if (b < ix.size()) {
-                ds = addr(objs[ix[b]].src) - addr(objs[ix[a]].src);
-                dc = addr(objs[ix[b]].coeffs) - addr(objs[ix[a]].coeffs);
-                dp = addr(objs[ix[b]].pieces) - addr(objs[ix[a]].pieces);
-                const bool ok = ds >= int64_t(k * ss) && dc >= int64_t(n * k) && dp >= int64_t(n * ps);
-                if (ok) {
-                    while (b < ix.size() && addr(objs[ix[b]].src) - addr(objs[ix[b - 1]].src) == ds &&
-                           addr(objs[ix[b]].coeffs) - addr(objs[ix[b - 1]].coeffs) == dc &&
-                           addr(objs[ix[b]].pieces) - addr(objs[ix[b - 1]].pieces) == dp && b - a < 0xFFFF)
-                        ++b;
-                } else {
-                    b = a + 1;
-                }
+    int st = ctx->activate();
+    if (st || (st = ctx->note_capture())) return st;
+    return ragged_matmul(ctx, jobs);
+}
+
+// Decoder::decode over pieces 0..m-1 + get_decoded_data (decoder.rs:96-177) for every object: the exact elimination
+// (one launch for the objects whose [coeffs | E] fits a wave's row, k + m <= 256, one for larger ones that fit LDS;
+// host threads for any beyond LDS), T × received data (the ragged matmul, <= 4 launches), the marker scan (1 launch)
+int rlnc_decode_ragged(rlnc_context *ctx, const rlnc_decode_object_desc *objs, size_t count, int32_t *piece_status_dev,
+                       int32_t *object_status_dev, int64_t *data_len_dev) {
+    CHECK_ARG(ctx != nullptr);
+    if (count == 0) return RLNC_OK;
+    CHECK_ARG(objs != nullptr && piece_status_dev && object_status_dev && data_len_dev && count <= 0x7FFFFFFF);
+    size_t tot_T = 0;
+    for (size_t i = 0; i < count; ++i) {
+        const rlnc_decode_object_desc &o = objs[i];
+        if (o.L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;  // decoder.rs:66-68
+        if (o.k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;   // :69-71
+        CHECK_ARG(o.pieces && o.decoded && o.m > 0 && o.m <= 0x7FFFFFFF && o.k <= 0x7FFFFFFF);
+        CHECK_ARG(o.piece_row_stride == 0 || o.piece_row_stride >= o.k + o.L);
+        tot_T += o.k * o.m;
+    }
+    int st = ctx->activate();
+    if (st || (st = ctx->note_capture())) return st;
+    if ((st = ctx->grow(ctx->ws_coef, tot_T)) || (st = ctx->grow(ctx->ws_rank, count * 4))) return st;
+    uint8_t *T = ctx->ws_coef.as<uint8_t>();
+    int32_t *rank = ctx->ws_rank.as<int32_t>();
+    // 1. the exact elimination
+    std::vector<rlnc::RrefObj> blk, wide;
+    std::vector<size_t> host, toff(count), soff(count);
+    size_t lds_blk = 0;
+    int hdr_lds = 1;
+    {
+        size_t to = 0, so = 0;
+        for (size_t i = 0; i < count; ++i) {
+            const rlnc_decode_object_desc &o = objs[i];
+            const int k = int(o.k), m = int(o.m);
+            const size_t ps = o.piece_row_stride ? o.piece_row_stride : o.k + o.L;
+            toff[i] = to;
+            soff[i] = so;
+            const rlnc::RrefObj r{o.pieces, int64_t(ps), T + to, piece_status_dev + so, rank + i, k, m};
+            if (rlnc::rref_block_eligible(k, m)) {
+                blk.push_back(r);
+                lds_blk = std::max(lds_blk, rlnc::rref_block_lds_bytes_public(k, m));
+            } else if (rlnc::rref_lds_bytes(k, m) <= rlnc::kRrefMaxLds) {
+                wide.push_back(r);
+                if (rlnc::rref_lds_bytes_staged_public(k, m) > rlnc::kRrefMaxLds) hdr_lds = 0;
+            } else {
+                host.push_back(i);
             }
-            const rlnc_object_desc &o = objs[ix[a]];
-            rlnc::MatmulParams p{};
-            p.in = o.src;
-            p.in_obj = ds;
-            p.in_row = int64_t(ss);
-            p.coef = o.coeffs;
-            p.coef_obj = dc;
-            p.coef_row = int64_t(k);
-            p.out = o.pieces + k;
-            p.out_obj = dp;
-            p.out_row = int64_t(ps);
-            p.hdr = o.pieces;
-            p.hdr_obj = dp;
-            p.hdr_row = int64_t(ps);
-            p.n_out = int(n);
-            p.n_in = int(k);
-            p.width = int64_t(L);
-            p.n_obj = int(b - a);
-            if ((st = ctx->matmul(p))) return st;
-            a = b;
+            to += o.k * o.m;
+            so += o.m;
         }
     }
+    size_t lds_wide = 0;  // one wide object's headers not fitting beside its matrix: none are staged
+    for (const auto &r : wide)
+        lds_wide = std::max(lds_wide, hdr_lds ? rlnc::rref_lds_bytes_staged_public(r.k, r.m) : rlnc::rref_lds_bytes(r.k, r.m));
+    if (!blk.empty() || !wide.empty()) {
+        std::vector<rlnc::RrefObj> tab(blk);
+        tab.insert(tab.end(), wide.begin(), wide.end());
+        void *dt = nullptr;
+        if ((st = upload_table(ctx, tab.data(), tab.size() * sizeof(rlnc::RrefObj), &dt))) return st;
+        const auto *t = static_cast<const rlnc::RrefObj *>(dt);
+        HIP_TRY(rlnc::launch_rref_ragged(t, int(blk.size()), true, lds_blk, 1, ctx->stream));
+        HIP_TRY(rlnc::launch_rref_ragged(t + blk.size(), int(wide.size()), false, lds_wide, hdr_lds, ctx->stream));
+    }
+    if (!host.empty()) {  // beyond LDS (k of several hundred): host threads' exact elimination, T and statuses uploaded
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_TRY(hipStreamIsCapturing(ctx->stream, &cs));
+        if (cs != hipStreamCaptureStatusNone)
+            return set_error(RLNC_ERR_INVALID_ARGUMENT, "a ragged decode with objects beyond LDS cannot be captured");
+        for (size_t i : host) {
+            const rlnc_decode_object_desc &o = objs[i];
+            const size_t ps = o.piece_row_stride ? o.piece_row_stride : o.k + o.L;
+            std::vector<uint8_t> hdr(o.m * o.k), Th(o.k * o.m, 0);
+            std::vector<int32_t> pst(o.m);
+            HIP_TRY(hipMemcpy2DAsync(hdr.data(), o.k, o.pieces, ps, o.k, o.m, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            rlnc::Elimination e(o.k, o.m);
+            for (size_t p = 0; p < o.m; ++p) {
+                int slot;
+                bool keep;
+                pst[p] = e.push(hdr.data() + p * o.k, &slot, &keep);
+            }
+            e.transform(Th.data(), o.m);
+            const int32_t r = int32_t(e.rank());
+            HIP_TRY(hipMemcpyAsync(T + toff[i], Th.data(), Th.size(), hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(hipMemcpyAsync(piece_status_dev + soff[i], pst.data(), o.m * 4, hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(hipMemcpyAsync(rank + i, &r, 4, hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));  // the host vectors go out of scope
+        }
+    }
+    // 2. decoded rows = T × received data rows
+    std::vector<MatmulJob> jobs;
+    jobs.reserve(count);
+    for (size_t i = 0; i < count; ++i) {
+        const rlnc_decode_object_desc &o = objs[i];
+        const int64_t ps = int64_t(o.piece_row_stride ? o.piece_row_stride : o.k + o.L);
+        jobs.push_back(MatmulJob{o.pieces + o.k, T + toff[i], o.decoded, nullptr, ps, int64_t(o.m), int64_t(o.L), 0,
+                                 int64_t(o.L), int(o.k), int(o.m)});
+    }
+    if ((st = ragged_matmul(ctx, jobs))) return st;
+    // 3. the marker scan
+    std::vector<ScanObj> scan(count);
+    for (size_t i = 0; i < count; ++i)
+        scan[i] = ScanObj{objs[i].decoded, rank + i, object_status_dev + i, data_len_dev + i,
+                          int64_t(objs[i].k * objs[i].L), int32_t(objs[i].k), 0};
+    void *ds = nullptr;
+    if ((st = upload_table(ctx, scan.data(), scan.size() * sizeof(ScanObj), &ds))) return st;
+    hipLaunchKernelGGL(ragged_final_len_kernel, dim3(unsigned(count)), dim3(64), 0, ctx->stream,
+                       static_cast<const ScanObj *>(ds));
+    HIP_TRY(hipGetLastError());
     return RLNC_OK;
 }
 
@@ -198,12 +499,18 @@ int rlnc_encoder_new_device(rlnc_context *ctx, const uint8_t *data_dev, size_t l
     uint8_t *img = nullptr;
     HIP_TRY(hipMalloc(&img, k * stride));
     rlnc_pad_desc d{data_dev, len, k, img, stride};
-    if ((st = rlnc_pad_batch_device(ctx, &d, 1)) || (st = encoder_adopt_device(ctx, img, k, L, stride, out))) {
-        (void)hipFree(img);
-        return st;
+    // pad, then wait for the image, then adopt it: a failed pad or sync leaves nothing behind (*out stays null)
+    if ((st = rlnc_pad_batch_device(ctx, &d, 1)) == RLNC_OK) {
+        const hipError_t e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess)
+            st = set_error(RLNC_ERR_DEVICE, "hipStreamSynchronize after the pad kernel: %s", hipGetErrorString(e));
     }
-    HIP_TRY(hipStreamSynchronize(ctx->stream));  // the image is complete when Encoder::new returns
-    return RLNC_OK;
+    if (st == RLNC_OK) st = encoder_adopt_device(ctx, img, k, L, stride, out);
+    if (st != RLNC_OK) {
+        (void)hipFree(img);
+        *out = nullptr;
+    }
+    return st;
 }
 
 }  // extern "C"

@@ -95,6 +95,31 @@ pub struct rlnc_object_desc {
     pub n: usize,
 }
 
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct rlnc_recode_object_desc {
+    pub pieces: *const u8,
+    pub piece_row_stride: usize,
+    pub r: *const u8,
+    pub out: *mut u8,
+    pub out_row_stride: usize,
+    pub k: usize,
+    pub L: usize,
+    pub n: usize,
+    pub n_recoded: usize,
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Debug)]
+pub struct rlnc_decode_object_desc {
+    pub pieces: *const u8,
+    pub piece_row_stride: usize,
+    pub decoded: *mut u8,
+    pub k: usize,
+    pub L: usize,
+    pub m: usize,
+}
+
 unsafe extern "C" {
     // status text, errors.rs:34-58
     pub fn rlnc_status_name(status: c_int) -> *const c_char;
@@ -349,6 +374,15 @@ unsafe extern "C" {
         out: *mut *mut rlnc_encoder,
     ) -> c_int;
     pub fn rlnc_encode_ragged(ctx: *mut rlnc_context, objs: *const rlnc_object_desc, count: usize) -> c_int;
+    pub fn rlnc_recode_ragged(ctx: *mut rlnc_context, objs: *const rlnc_recode_object_desc, count: usize) -> c_int;
+    pub fn rlnc_decode_ragged(
+        ctx: *mut rlnc_context,
+        objs: *const rlnc_decode_object_desc,
+        count: usize,
+        piece_status_dev: *mut i32,
+        object_status_dev: *mut i32,
+        data_len_dev: *mut i64,
+    ) -> c_int;
 
     // host-resident pieces (pinned or pageable host buffers)
     pub fn rlnc_encode_host_stream(

@@ -1,4 +1,6 @@
 """Helpers for the -m gpu tests: a vectorised numpy GF(2^8) matmul as the independent CPU checker."""
+import os
+
 import numpy as np
 
 from oracle import np_oracle as npo
@@ -27,3 +29,19 @@ def host(t) -> np.ndarray:
 
     torch.cuda.synchronize()
     return t.cpu().numpy()
+
+
+# The shipped library carries matmul variants 0, 1, 6, 7, 8 and decode paths 0, 1, 2, 5; the A/B history (variants
+# 2-5 and 9, decode paths 3, 4, 6) is in the diagnostic build only (make -C rlnc_amd/csrc ab), which the variant
+# tests cover when RLNC_LIB_PATH points at it.
+AB_BUILD = os.path.basename(os.environ.get("RLNC_LIB_PATH", "")) == "librlnc_hip_ab.so"
+MATMUL_AB_ONLY = {2, 3, 4, 5, 9}
+DECODE_AB_ONLY = {3, 4, 6}
+
+
+def variants(*vals):
+    return [v for v in vals if AB_BUILD or v not in MATMUL_AB_ONLY]
+
+
+def decode_paths(*vals):
+    return [v for v in vals if AB_BUILD or v not in DECODE_AB_ONLY]

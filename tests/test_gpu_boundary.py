@@ -216,3 +216,28 @@ def test_variant8_strided_with_header(ctx, n_out):
         assert np.array_equal(got[o, :, :n_in], coef[o])
         assert np.array_equal(got[o, :, 64:64 + W], np_matmul(coef[o], inp[o, :, :W]))
         assert not got[o, :, 64 + W:].any() and not got[o, :, n_in:64].any()
+
+
+def test_stream_contexts_stay_bounded():
+    """batch calls without an explicit context on many torch streams keep at most STREAM_CONTEXTS_PER_THREAD
+    default contexts per thread (each holds grow-only workspaces), and every call stays correct."""
+    import torch
+
+    from rlnc_amd import batch, context
+    from tests.gpu_util import dev, host, np_matmul
+
+    rng = np.random.default_rng(21)
+    src = rng.integers(0, 256, (1, 8, 4096), dtype=np.uint8)
+    co = rng.integers(0, 256, (1, 12, 8), dtype=np.uint8)
+    want = np_matmul(co[0], src[0])
+    streams = [torch.cuda.Stream() for _ in range(12)]
+    for rep in range(2):
+        for s in streams:
+            with torch.cuda.stream(s):
+                out = torch.zeros((1, 12, 8 + 4096), dtype=torch.uint8, device="cuda:0")
+                batch.encode_batch(dev(src), dev(co), out)
+            s.synchronize()
+            assert np.array_equal(host(out)[0, :, 8:], want)
+            assert len(context._tls.sctxs) <= context.STREAM_CONTEXTS_PER_THREAD
+    context.release_stream_contexts()
+    assert len(context._tls.sctxs) == 0

@@ -79,3 +79,90 @@ def test_encode_batch_under_graph_capture_first_use(variant):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "graph ok" in r.stdout
+
+
+# Descriptor tables under capture (wire.hip upload_table): a captured pad call and a captured ragged decode keep
+# their own tables, so eager calls with OTHER descriptors between the capture and a replay cannot change what the
+# replay reads (the captured tables are written by kernels that carry the bytes, into a region never reused).
+CHILD_TABLES = r"""
+import sys
+sys.path.insert(0, ROOT)
+import ctypes as C
+import numpy as np
+import torch
+import rlnc_amd
+from rlnc_amd import _lib, batch
+from oracle.oracle import Oracle
+
+orc = Oracle()
+ctx = rlnc_amd.Context(0)
+rng = np.random.default_rng(11)
+shapes = [(1000, 3), (5000, 16), (4096 * 2 - 1, 2)]
+
+
+def pad_set():
+    datas = [torch.from_numpy(rng.integers(0, 256, n, dtype=np.uint8)).cuda() for n, _ in shapes]
+    outs = [torch.zeros(k * orc.piece_byte_len(n, k), dtype=torch.uint8, device="cuda") for n, k in shapes]
+    arr = (_lib.PadDesc * len(shapes))(*[_lib.PadDesc(d.data_ptr(), n, k, o.data_ptr(), 0)
+                                         for (n, k), d, o in zip(shapes, datas, outs)])
+    return datas, outs, arr
+
+
+def decode_set(B=6):
+    objs, srcs = [], []
+    for o in range(B):
+        k, L = (16, 4096) if o % 2 else (40, 3 * 4096 + 16)
+        src = orc.pad(rng.integers(0, 256, k * L - 3, dtype=np.uint8), k)
+        pc = torch.from_numpy(orc.encode(src, rng.integers(0, 256, (k + 2, k), dtype=np.uint8))).cuda()
+        objs.append((pc, k, torch.zeros((k, L), dtype=torch.uint8, device="cuda")))
+        srcs.append(src)
+    return objs, srcs
+
+
+def pad(arr):
+    ctx.use_torch_stream()
+    assert ctx.lib.rlnc_pad_batch_device(ctx.h, arr, len(shapes)) == 0
+
+
+X = pad_set()
+A = decode_set()
+pad(X[2])  # eager warm-up: workspaces, the capture arena, the block-table probe
+batch.decode_ragged(A[0], ctx)
+torch.cuda.synchronize()
+s = torch.cuda.Stream()
+with torch.cuda.stream(s):
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        pad(X[2])
+        res = batch.decode_ragged(A[0], ctx)
+torch.cuda.synchronize()
+Y = pad_set()  # other descriptors, same sizes, eager, between the capture and the replay
+B_ = decode_set()
+pad(Y[2])
+resB = batch.decode_ragged(B_[0], ctx)
+torch.cuda.synchronize()
+for (n, k), d, o in zip(shapes, Y[0], Y[1]):
+    assert np.array_equal(o.cpu().numpy(), orc.pad(d.cpu().numpy(), k).reshape(-1)), "eager pad"
+for (pc, k, dec), src in zip(B_[0], B_[1]):
+    assert np.array_equal(dec.cpu().numpy(), src), "eager ragged decode"
+for o in X[1]:
+    o.zero_()
+for _, _, dec in A[0]:
+    dec.zero_()
+res[1].fill_(-1)
+g.replay()
+torch.cuda.synchronize()
+for (n, k), d, o in zip(shapes, X[0], X[1]):
+    assert np.array_equal(o.cpu().numpy(), orc.pad(d.cpu().numpy(), k).reshape(-1)), "replayed pad"
+for (pc, k, dec), src in zip(A[0], A[1]):
+    assert np.array_equal(dec.cpu().numpy(), src), "replayed ragged decode"
+assert (res[1].cpu().numpy() == 0).all(), "replayed statuses"
+print("tables ok")
+"""
+
+
+def test_descriptor_tables_survive_other_eager_calls_before_replay():
+    code = CHILD_TABLES.replace("ROOT", repr(ROOT))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "tables ok" in r.stdout
