@@ -42,6 +42,11 @@ METRIC = "device-resident RLNC encode+decode GiB/s, k=32 × 1 MiB, at 1/2/4/8 MI
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GIB = float(1 << 30)
 MA_PER_XOR3 = 256  # GF(2^8) multiply-adds per v_bitop3 XOR3 of the bit-sliced kernel (measure/gf_ceiling.hip)
+# the guide's VALU issue spec (MI355X_MICROARCH.md): 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per
+# SIMD at 2.4 GHz -> 1.2288 T XOR3/s x 256 multiply-adds = 314.6 T GF(2^8) multiply-adds/s
+SPEC_XOR3_PER_S = 256 * 4 * 2.4e9 / 2
+SPEC_PEAK_T_MA = SPEC_XOR3_PER_S * MA_PER_XOR3 / 1e12
+CPU_SHARE = 16  # host cores per GPU on the GPU box (os.cpu_count() there shows the whole machine)
 
 WORKLOADS = {
     # name: k, L, coded n, decoded-from m, objects (per rank for config2, whole job for config5), chunk
@@ -99,12 +104,21 @@ class Dist:
         self.pg = None
 
     def init(self, backend: str):
-        if self.world > 1:
-            import torch.distributed as dist
+        """Initialise the process group (RCCL for the GPU run, gloo for the CPU harness test) -- at world size 1
+        too, on a free 127.0.0.1 port, so that every line reports the world size the group initialised with."""
+        import torch.distributed as dist
 
-            dist.init_process_group(backend=backend)
-            self.pg = dist
+        if self.world == 1 and "MASTER_PORT" not in os.environ:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ["MASTER_PORT"] = str(_free_port())
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        dist.init_process_group(backend=backend)
+        self.pg = dist
         return self
+
+    def initialised_world(self) -> int:
+        return self.pg.get_world_size() if self.pg else 0
 
     def barrier(self):
         if self.pg:
@@ -301,10 +315,11 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default 30 for config2, 5 for config5)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 5 for config2, 2 for config5)")
-    ap.add_argument("--workload", choices=sorted(WORKLOADS) + ["oracle-cpu"], default="config2",
+    ap.add_argument("--workload", choices=sorted(WORKLOADS) + ["oracle-cpu", "oracle-cpu-config5"], default="config2",
                     help="config2: the metric's shape, objects per GPU (weak scaling); config5: BASELINE configs[4], "
-                         "4,096 objects split over the ranks (strong scaling); oracle-cpu: the harness alone with "
-                         "the C oracle as each rank's work and gloo (tests)")
+                         "4,096 objects split over the ranks (strong scaling); oracle-cpu / oracle-cpu-config5: the "
+                         "harness alone with the C oracle as each rank's work and gloo (tests), per-rank objects / "
+                         "a fixed job split over the ranks")
     ap.add_argument("--objects", type=int, default=None,
                     help="config2: objects per GPU per step (32: profiles/r01_launch_size.txt); config5: the whole job")
     ap.add_argument("--k", type=int, default=None)
@@ -317,8 +332,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the live XOR3-issue ceiling microbenchmark")
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="threads of the all-cores CPU baseline (one object each; the box's share is 16 cores per GPU)")
+    ap.add_argument("--cpu-threads", type=int, default=CPU_SHARE,
+                    help="threads of the CPU-share baseline (one object each; the GPU box grants 16 host cores per GPU)")
     ap.add_argument("--encode-only", action="store_true", help="diagnostic: time only the encode launch")
     ap.add_argument("--pipeline", type=int, default=2,
                     help="1: the decoder's elimination (reads only the coded pieces' coefficient headers, written "
@@ -352,7 +367,7 @@ def main():
         sys.exit(5)
     assert dist.world == args.gpus or (dist.world == 1 and args.gpus == 1), \
         f"--gpus {args.gpus} but WORLD_SIZE={dist.world}"
-    if args.workload == "oracle-cpu":
+    if args.workload.startswith("oracle-cpu"):
         return run_oracle_cpu(args, dist)
     return run_gpu(args, dist)
 
@@ -367,6 +382,10 @@ def run_oracle_cpu(args, dist: Dist):
     dist.init("gloo")
     orc = Oracle()
     k, L, n, m, B = 8, 512, 12, 8, 3
+    strong = args.workload == "oracle-cpu-config5"
+    if strong:  # config5's split: a fixed job of J objects over the ranks (the first J % N ranks take one more)
+        J = args.objects or 7
+        B = J // dist.world + (1 if dist.rank < J % dist.world else 0)
     rng = np.random.default_rng(100 + dist.rank)  # each rank owns different objects
     src = rng.integers(0, 256, (B, k, L), dtype=np.uint8)
     co = rng.integers(0, 256, (B, n, k), dtype=np.uint8)
@@ -384,13 +403,17 @@ def run_oracle_cpu(args, dist: Dist):
 
     elapsed = timed_loop(step, args.steps, args.warmup, dist, lambda: None)
     total = dist.allreduce(float(step_bytes(B, k, L, n) * args.steps), "sum")
+    total_objs = dist.allreduce(float(B), "sum")
     ok = dist.allreduce(float(all(np.array_equal(last[o], src[o]) for o in range(B))), "sum") == dist.world
     if dist.rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(total / elapsed / GIB, 6), "unit": "GiB/s",
-                          "n_gpus": dist.world, "steps": args.steps, "warmup": args.warmup,
+                          "n_gpus": dist.world, "world_size_initialised": dist.initialised_world(),
+                          "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
-                          "scaling": "weak", "elapsed_s": elapsed, "total_bytes": total, "verified": bool(ok),
-                          "config": {"workload": "oracle-cpu harness test"}}), flush=True)
+                          "scaling": "strong" if strong else "weak", "elapsed_s": elapsed, "total_bytes": total,
+                          "verified": bool(ok), "objects_total": int(total_objs), "objects_rank0": B,
+                          "config": {"workload": "oracle-cpu harness test" + (" (fixed job split)" if strong else "")}}),
+              flush=True)
     dist.close()
     if not ok:
         sys.exit(3)
@@ -600,6 +623,10 @@ def run_gpu(args, dist: Dist):
         "peak": peak,
         "unit": "T GF(2^8) multiply-adds/s",
         "frac": round(achieved / peak, 4) if peak else None,
+        # the same against the guide's issue spec (2 cycles per wave64 VALU instruction at 2.4 GHz), not the live
+        # ceiling: the live XOR3 rate is 0.75-0.77 of spec (clock under load, 3-source issue), so frac_spec < frac
+        "peak_spec": round(SPEC_PEAK_T_MA, 2),
+        "frac_spec": round(achieved / SPEC_PEAK_T_MA, 4),
         "traffic": traffic,
         "traffic_source": traffic_src,
         "kernel": f"{KERNELS[variant]} (encode: {n} coded pieces x {B} objects per launch)",
@@ -654,6 +681,7 @@ def run_gpu(args, dist: Dist):
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": dist.world,
+        "world_size_initialised": dist.initialised_world(),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
@@ -694,10 +722,16 @@ def run_gpu(args, dist: Dist):
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(k, L, n, m, args.cpu_seconds)
         result["vs_cpu_baseline"] = round(value / result["cpu_baseline"]["value"], 1)
-        if args.cpu_threads > 1:  # the same on the box's CPU share (16 cores per GPU), one object per thread
+        if args.cpu_threads > 1:
+            # the same on the host cores one GPU gets on the box (16; os.cpu_count() there is the whole machine's,
+            # which this process may not use), one object per thread
             threads = min(args.cpu_threads, os.cpu_count() or 1)
-            result["cpu_baseline_all_cores"] = cpu_baseline(k, L, n, m, args.cpu_seconds, threads)
-            result["vs_cpu_baseline_all_cores"] = round(value / result["cpu_baseline_all_cores"]["value"], 1)
+            share = cpu_baseline(k, L, n, m, args.cpu_seconds, threads)
+            share["host_cpus_visible"] = os.cpu_count()
+            share["note"] = (f"{threads} threads = the GPU box's host-core share per GPU; the machine shows "
+                             f"{os.cpu_count()} CPUs, shared by its 8 GPUs' jobs")
+            result["cpu_baseline_cpu_share"] = share
+            result["vs_cpu_baseline_cpu_share"] = round(value / share["value"], 1)
     if dist.rank == 0:
         print(json.dumps(result), flush=True)
     dist.close()

@@ -101,6 +101,7 @@ def test_self_spawn_two_ranks_gloo():
     assert len(lines) == 1, r.stdout  # rank 0 only
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["steps"] == 3 and res["verified"]
+    assert res["world_size_initialised"] == 2  # torch.distributed.get_world_size() after init_process_group
     assert res["total_bytes"] == 2 * bench.step_bytes(3, 8, 512, 12) * 3
     assert abs(res["value"] - res["total_bytes"] / res["elapsed_s"] / bench.GIB) < 1e-3
 
@@ -129,3 +130,40 @@ def test_config5_split_is_a_fixed_job():
     for n in (1, 2, 3, 4, 8):
         per = [a.objects // n + (1 if r < a.objects % n else 0) for r in range(n)]
         assert sum(per) == 4096
+
+
+def test_self_spawn_two_ranks_config5_split():
+    """`--workload config5` is one fixed job split over the ranks (strong scaling): the same self-spawned harness
+    with the oracle stand-in (`oracle-cpu-config5`), a job of 7 objects over 2 ranks (4 + 3)."""
+    import json
+    import subprocess
+    import sys
+
+    import bench
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py"), "--gpus", "2",
+                        "--workload", "oracle-cpu-config5", "--objects", "7", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["scaling"] == "strong" and res["world_size_initialised"] == 2 and res["verified"]
+    assert res["objects_total"] == 7 and res["objects_rank0"] == 4
+    assert res["total_bytes"] == bench.step_bytes(7, 8, 512, 12) * 2
+
+
+def test_single_rank_initialises_a_group():
+    """N = 1 also reports the world size its process group initialised with (a free 127.0.0.1 port)."""
+    import json
+    import subprocess
+    import sys
+
+    import bench
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py"),
+                        "--workload", "oracle-cpu", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["n_gpus"] == 1 and res["world_size_initialised"] == 1
