@@ -102,19 +102,30 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         self.pg = None
+        self.bar = None
 
     def init(self, backend: str):
-        """Initialise the process group (RCCL for the GPU run, gloo for the CPU harness test) -- at world size 1
-        too, on a free 127.0.0.1 port, so that every line reports the world size the group initialised with."""
+        """Initialise the process group (RCCL for the multi-GPU run, gloo for the CPU harness test) -- at world size
+        1 too, on a free 127.0.0.1 port, so that every line reports the world size the group initialised with.  A
+        single rank takes gloo: its barrier and reductions then stay on the host, and RCCL's own streams do not
+        share the 4 hardware queues (GPU_MAX_HW_QUEUES) with the bench's three pipeline streams (with an RCCL group
+        at N = 1 the pipelined step measured 4-5 % slower at equal kernel times)."""
         import torch.distributed as dist
 
-        if self.world == 1 and "MASTER_PORT" not in os.environ:
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ["MASTER_PORT"] = str(_free_port())
-            os.environ.setdefault("RANK", "0")
-            os.environ.setdefault("WORLD_SIZE", "1")
+        if self.world == 1:
+            backend = "gloo"
+            if "MASTER_PORT" not in os.environ:
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ["MASTER_PORT"] = str(_free_port())
+                os.environ.setdefault("RANK", "0")
+                os.environ.setdefault("WORLD_SIZE", "1")
+        backend = os.environ.get("RLNC_BENCH_PG", backend)  # diagnostic override of the group's backend
         dist.init_process_group(backend=backend)
         self.pg = dist
+        # the timing barrier on a host (gloo) group: every rank has synchronised its device just before, so a
+        # host barrier orders the ranks; an RCCL barrier inside the timed region measured ~3.5 ms per call at
+        # N = 1 (torch's NCCL barrier is an allreduce plus a device-wide wait), i.e. 7 % of a 30-step run
+        self.bar = dist.new_group(backend="gloo") if backend == "nccl" else None
         return self
 
     def initialised_world(self) -> int:
@@ -122,7 +133,7 @@ class Dist:
 
     def barrier(self):
         if self.pg:
-            self.pg.barrier()
+            self.pg.barrier(group=self.bar)
 
     def allreduce(self, value: float, op: str) -> float:
         if not self.pg:
@@ -682,6 +693,7 @@ def run_gpu(args, dist: Dist):
         "unit": "GiB/s",
         "n_gpus": dist.world,
         "world_size_initialised": dist.initialised_world(),
+        "process_group_backend": dist.pg.get_backend() if dist.pg else None,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
