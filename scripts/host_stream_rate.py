@@ -59,6 +59,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--window", type=int, default=0, help="objects per pipeline window (0 = library default)")
     ap.add_argument("--no-numa-bind", action="store_true", help="do not pin the process to the GPU's NUMA node")
+    ap.add_argument("--modes", default="pinned,pageable,concurrent,raw",
+                    help="comma list of pinned, pageable, concurrent, raw (the box's raw copy rates)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -75,7 +77,8 @@ def main():
                      "k=32 x 1 MiB", "unit": "GiB/s", "objects": B,
            "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)"),
            "numa_node_bound": node, "cpus": len(os.sched_getaffinity(0))}
-    for mode in ("pinned", "pageable"):
+    modes = set(args.modes.split(","))
+    for mode in [x for x in ("pinned", "pageable") if x in modes]:
         pin = mode == "pinned"
 
         def buf(shape):
@@ -105,8 +108,11 @@ def main():
         step()  # warm-up: the library's pipeline buffers are allocated once and kept
         part["encode"] = part["decode"] = 0.0
         t0 = time.perf_counter()
+        per_step = []
         for _ in range(args.steps):
+            ts = time.perf_counter()
             step()
+            per_step.append(round((time.perf_counter() - ts) * 1e3, 2))
         el = (time.perf_counter() - t0) / args.steps
         ok = all((ps[o] == 0).sum() < k or np.array_equal(dec.numpy()[o], src.numpy()[o]) for o in range(B))
         moved = B * (k * L + n * k + n * (k + L) + m * (k + L) + k * L)
@@ -116,12 +122,16 @@ def main():
                      "encode_call_ms": round(part["encode"] / args.steps * 1e3, 2),
                      "encode_call_GBps": round(B * (k * L + n * k + n * (k + L)) / (part["encode"] / args.steps) / 1e9, 2),
                      "decode_call_ms": round(part["decode"] / args.steps * 1e3, 2),
-                     "decode_call_GBps": round(B * (m * (k + L) + k * L) / (part["decode"] / args.steps) / 1e9, 2)}
+                     "decode_call_GBps": round(B * (m * (k + L) + k * L) / (part["decode"] / args.steps) / 1e9, 2),
+                     "step_ms": per_step}
         del src, co, pieces, dec
     # concurrent: step i's encode (thread A, context A) beside step i-1's decode (thread B, context B); ctypes releases
     # the GIL inside the library, so the two calls overlap on the device and on PCIe
     import threading
 
+    if "concurrent" not in modes:
+        print(json.dumps(out), flush=True)
+        return
     ctx2 = rlnc_amd.Context(0)
     buf = lambda shape: torch.empty(shape, dtype=torch.uint8, pin_memory=True)
     src, co = buf((B, k, L)), buf((B, n, k))
