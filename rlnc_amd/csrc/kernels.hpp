@@ -112,6 +112,12 @@ struct RrefParams {
     int lds_only;  // clean-state path (A/B, all exact): 0 auto (blocked clean run when k + m <= 256, else 4);
                    // 1 LDS; 2 registers, one wave; 3 blocked clean run (gf_rref_block_kernel); 4 registers, multi-wave
     const struct RrefObj *objs = nullptr;  // ragged batch: object o's shape and buffers (the fields above unused)
+    // two-pass elimination when k + m > 256 (k <= 128): pass 1 (the blocked run) replays only the first m pieces of
+    // each object with statuses / T at row stride m_stride (> m): an object full-ranked within them is exact
+    // (decode() answers ReceivedAllPieces for every later piece and leaves the state alone, decoder.rs:97-99); pass 2
+    // (the general kernel over all pieces) skips the objects pass 1 full-ranked (skip_full) and redoes the others
+    int m_stride = 0;   // 0 = m
+    int skip_full = 0;
 };
 // One object of a ragged elimination launch (rlnc_decode_ragged): T is k x m row-major, status m entries.
 struct RrefObj {
@@ -120,7 +126,9 @@ struct RrefObj {
     uint8_t *T;
     int32_t *status;
     int32_t *rank;
-    int32_t k, m;
+    int32_t k, m;      // m = received pieces (the row stride of T and of the statuses)
+    int32_t m_first;   // > 0: the blocked pass replays only the first m_first pieces (see RrefParams::m_stride)
+    int32_t two_pass;  // the general pass skips this object when the blocked pass full-ranked it
 };
 // ragged elimination: one workgroup per object of the device table objs (n objects, k + m <= 256 each when
 // block = true -- the blocked clean run -- else the one-wave LDS kernel); lds = the largest object's need

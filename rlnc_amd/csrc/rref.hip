@@ -697,6 +697,12 @@ __device__ __forceinline__ void rref_ragged_object(RrefParams &p, int &o) {
     p.piece_stride = d.piece_stride;
     p.k = __builtin_amdgcn_readfirstlane(d.k);
     p.m = __builtin_amdgcn_readfirstlane(d.m);
+    p.m_stride = 0;
+    if (!p.skip_full && d.m_first > 0) {  // the blocked pass over the first pieces only
+        p.m = __builtin_amdgcn_readfirstlane(d.m_first);
+        p.m_stride = __builtin_amdgcn_readfirstlane(d.m);
+    }
+    p.skip_full = p.skip_full && d.two_pass;
     p.T = d.T;
     p.T_obj = 0;
     p.status = d.status;
@@ -712,6 +718,7 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, in
     const int tid = threadIdx.x;
     int o = blockIdx.x;
     rref_ragged_object(p, o);
+    if (p.skip_full && p.rank[o] >= p.k) return;  // two-pass: the blocked pass already full-ranked this object
     const int k = p.k, m = p.m;
 #ifdef RLNC_RREF_PROFILE  // diagnostic build: statuses become per-piece cycle counts, rank the setup cycles
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
@@ -1354,12 +1361,16 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
         for (int i = 0; i < 8 && i < m; ++i) St[i] = int32_t(bprof[i]);
     __syncthreads();
 #endif
-    for (int q = tid; q < m; q += 64 * NW) p.status[int64_t(o) * m + q] = St[q];
+    // two-pass (m_stride > m): the pieces after the first m are ReceivedAllPieces when they full-ranked the object
+    // (decoder.rs:97-99, no state change), else the general pass rewrites this object; their T columns are zero
+    const int ms = p.m_stride > m ? p.m_stride : m;
+    for (int q = tid; q < ms; q += 64 * NW)
+        p.status[int64_t(o) * ms + q] = q < m ? St[q] : (rows == k ? RLNC_ERR_RECEIVED_ALL_PIECES : -1);
     if (tid == 0) p.rank[o] = rows;
     uint8_t *T = p.T + int64_t(o) * p.T_obj;
-    for (int e = tid; e < k * m; e += 64 * NW) {
-        const int rr = e / m, s2 = e % m;
-        T[e] = rr < rows ? M.b[rr * M.S + k + s2] : uint8_t(0);
+    for (int e = tid; e < k * ms; e += 64 * NW) {
+        const int rr = e / ms, s2 = e % ms;
+        T[e] = rr < rows && s2 < m ? M.b[rr * M.S + k + s2] : uint8_t(0);
     }
 }
 
@@ -1394,6 +1405,7 @@ hipError_t launch_rref_ragged(const RrefObj *objs, int n, bool block, size_t lds
     RrefParams p{};
     p.objs = objs;
     p.n_obj = n;
+    p.skip_full = block ? 0 : 1;  // the general launch skips two-pass objects the blocked launch full-ranked
     // the dynamic-LDS attribute of both kernels (a first launch through launch_rref_batch may not have run yet)
     static std::mutex mu;
     static bool attr_set[64] = {};
@@ -1420,8 +1432,29 @@ hipError_t launch_rref_ragged(const RrefObj *objs, int n, bool block, size_t lds
     return hipGetLastError();
 }
 
+static hipError_t launch_rref_one(const RrefParams &p, hipStream_t s);
+
+// k + m > 256 with k <= 128: the blocked run over the first 256 - k pieces (>= k), then the general kernel over all m
+// pieces for the objects that did not reach rank k within them (with dense coefficients: none).  Same outputs as the
+// general kernel alone (RrefParams::m_stride); 32 objects of k = 128, m = 130: 4.0 ms in the one-wave LDS kernel.
 hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
     if (p.n_obj <= 0) return hipSuccess;
+    if (p.lds_only == 0 && p.objs == nullptr && p.m_stride == 0 && !p.skip_full && p.k <= 128 &&
+        rref_row_dwords(p.k, p.m) > 64 && rref_lds_bytes(p.k, p.m) <= kRrefMaxLds &&
+        rref_block_lds_bytes(p.k, 256 - p.k) <= kRrefMaxLds) {
+        RrefParams a = p;
+        a.m = 256 - p.k;
+        a.m_stride = p.m;
+        hipError_t e = launch_rref_one(a, s);
+        if (e != hipSuccess) return e;
+        RrefParams b = p;
+        b.skip_full = 1;
+        return launch_rref_one(b, s);
+    }
+    return launch_rref_one(p, s);
+}
+
+static hipError_t launch_rref_one(const RrefParams &p, hipStream_t s) {
     // many small objects (k <= 16, >= 2048 of them: 8 per CU and more): the one-wave register kernel (path 4's)
     // beats the 4-wave blocked run, whose per-object parallelism the full grid no longer needs -- 4,096 x k = 16:
     // 0.093 vs 0.125 ms, k = 8: 0.051 vs 0.067, k = 16 sparse + dependent: 0.195 vs 0.295; at 512 objects the

@@ -411,11 +411,19 @@ int rlnc_decode_ragged(rlnc_context *ctx, const rlnc_decode_object_desc *objs, s
             const size_t ps = o.piece_row_stride ? o.piece_row_stride : o.k + o.L;
             toff[i] = to;
             soff[i] = so;
-            const rlnc::RrefObj r{o.pieces, int64_t(ps), T + to, piece_status_dev + so, rank + i, k, m};
+            rlnc::RrefObj r{o.pieces, int64_t(ps), T + to, piece_status_dev + so, rank + i, k, m, 0, 0};
             if (rlnc::rref_block_eligible(k, m)) {
                 blk.push_back(r);
                 lds_blk = std::max(lds_blk, rlnc::rref_block_lds_bytes_public(k, m));
             } else if (rlnc::rref_lds_bytes(k, m) <= rlnc::kRrefMaxLds) {
+                // k <= 128: the blocked run over the first 256 - k pieces, the general kernel only for an object
+                // that did not reach rank k within them (rref.hip launch_rref_batch, two passes)
+                if (k <= 128 && rlnc::rref_block_eligible(k, 256 - k)) {
+                    r.m_first = 256 - k;
+                    r.two_pass = 1;
+                    blk.push_back(r);
+                    lds_blk = std::max(lds_blk, rlnc::rref_block_lds_bytes_public(k, 256 - k));
+                }
                 wide.push_back(r);
                 if (rlnc::rref_lds_bytes_staged_public(k, m) > rlnc::kRrefMaxLds) hdr_lds = 0;
             } else {

@@ -810,3 +810,46 @@ def test_decode_many_small_objects(ctx, k, m, sparsity, dep):
         assert np.array_equal(got[o, : pay.shape[0]], pay), o
         st, _ = od.get_decoded_data()
         assert S[ost[o]] == S[st], o
+
+
+@pytest.mark.parametrize("path", [0, 2])
+def test_decode_two_pass_beyond_one_wave_row(ctx, path):
+    """k + m > 256 with k <= 128: the blocked run over the first 256 - k pieces, the general kernel only for objects
+    not full-ranked within them (rref.hip launch_rref_batch).  Objects 0-3 reach rank k early (the later pieces are
+    ReceivedAllPieces, T columns zero); objects 4-5 have their first 256 - k pieces spanning only 40 dimensions, so
+    the general pass must redo them over all m pieces; object 6 never reaches rank k."""
+    from rlnc_amd import batch
+
+    from oracle.oracle import Oracle
+
+    orc = Oracle()
+    rng = np.random.default_rng(4242)
+    k, m, L, nobj = 64, 230, 24, 7
+    first = 256 - k
+    seqs = np.zeros((nobj, m, k + L), np.uint8)
+    for o in range(nobj):
+        src = rng.integers(0, 256, (k, L), dtype=np.uint8)
+        co = rng.integers(0, 256, (m, k), dtype=np.uint8)
+        if o >= 4:
+            base = rng.integers(0, 256, (40, k), dtype=np.uint8)
+            co[:first] = orc.encode(base, rng.integers(0, 256, (first, 40), dtype=np.uint8))[:, 40:]
+        if o == 6:
+            co[first:] = orc.encode(co[:8], rng.integers(0, 256, (m - first, 8), dtype=np.uint8))[:, 8:]
+        seqs[o] = orc.encode(src, co)
+    decoded = dev(np.zeros((nobj, k, L), np.uint8))
+    ctx.set_decode_path(path)
+    try:
+        pst, ost, dl = batch.decode_batch(dev(seqs), k, decoded, ctx)
+    finally:
+        ctx.set_decode_path(0)
+    got = host(decoded)
+    for o in range(nobj):
+        od = OracleDecoder(L, k)
+        want = [S[od.decode(p)] for p in seqs[o]]
+        assert [S[x] for x in pst[o]] == want, o
+        pay = od.padded_payload()
+        assert np.array_equal(got[o, : pay.shape[0]], pay), o
+        st, _ = od.get_decoded_data()
+        assert S[ost[o]] == S[st], o
+    assert all(S[x] == "ReceivedAllPieces" for x in pst[0, first:])
+    assert (pst[4] == 0).sum() == k and (pst[6] == 0).sum() < k

@@ -22,7 +22,8 @@ DECODE_SHAPES = [
     (100, 2 * 4096, 110, 20, 0.05, 0.5, 16),
     (128, 8192, 128, 16, 0.0, 0.0, 0),
     (8, 64, 6, 24, 0.0, 0.0, 0),  # m < k: NotAllPiecesReceivedYet
-    (200, 4096, 204, 4, 0.0, 0.0, 0),  # k + m > 256: the one-wave LDS kernel
+    (200, 4096, 204, 4, 0.0, 0.0, 0),  # k + m > 256, k > 128: the one-wave LDS kernel
+    (100, 4096 + 32, 180, 6, 0.1, 0.6, 0),  # k + m > 256, k <= 128: blocked run over 156 pieces, general pass if needed
     (400, 64, 402, 2, 0.0, 0.0, 0),  # beyond LDS: host threads
 ]
 
