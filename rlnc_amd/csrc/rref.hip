@@ -137,15 +137,19 @@ struct Mat {
     __device__ uint32_t at(int r, int c) const { return b[r * S + c]; }
 };
 
+// lane within the wave: the single-wave helpers below also run in one wave of a multi-object workgroup
+__device__ __forceinline__ int lane_id() { return int(threadIdx.x & 63u); }
+
 // row_t[c >= c0] ^= q · row_s[c >= c0]   (simd/mod.rs:89-119 on the byte range of decoder_matrix.rs:158-161)
 __device__ __forceinline__ void row_muladd(const Mat &M, const uint32_t *tab, int t, int s, uint32_t q, int c0) {
-    for (int w = threadIdx.x; w < M.D; w += 64) {
+    for (int w = lane_id(); w < M.D; w += 64) {
         const uint32_t mask = from_mask(w, c0);
         if (mask) M.w[t * M.D + w] ^= mul4(tab, q, M.w[s * M.D + w]) & mask;
     }
 }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
 
 // WG: a workgroup barrier; else the code runs in one wave only (the other waves of the workgroup are elsewhere and
 // must not be waited for): a compiler fence suffices, a wave's LDS operations execute in issue order
@@ -163,7 +167,7 @@ __device__ __forceinline__ void rsync() {
 // DecoderMatrix::rref — decoder_matrix.rs:99-244, verbatim.  Returns the new row count.
 template <bool WG = true>
 __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     // clean_forward :120-166 (boundary = min(rows, cols) = rows, since rows <= k < cols)
     for (int i = 0; i < R; ++i) {
         uint32_t piv = M.at(i, i);
@@ -252,7 +256,7 @@ __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
 
 // rows 0..R-1 a clean RREF: M[i][i] = 1 and column i zero in every other row (i < R)
 __device__ bool is_clean(const Mat &M, int R) {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     bool ok = true;
     for (int g = 0; g < R; g += 64) {
         const int j = g + lane;
@@ -387,22 +391,22 @@ __device__ int clean_append(const Mat &M, const uint32_t *tab, int r, int k, boo
 //   normalise from column r+1 (:200-211), byte r := 1;
 //   backward (:179-198) every row j < r ^= M[j][r]·row_r, M[j][r] broadcast from lane (r/4, g).
 // ---------------------------------------------------------------------------------------------------
-template <int G, int RT>
+template <int G, int RT, bool WG = true>
 __device__ void regs_to_lds(const Mat &M, const uint32_t (&v)[RT], int rows) {
     constexpr int DP = 64 / G;
-    const int w = threadIdx.x % DP, g = threadIdx.x / DP;
+    const int w = lane_id() % DP, g = lane_id() / DP;
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
         const int row = G * t + g;
         if (row < rows && w < M.D) M.w[row * M.D + w] = v[t];
     }
-    __syncthreads();
+    rsync<WG>();
 }
 
 template <int G, int RT>
 __device__ void lds_to_regs(const Mat &M, uint32_t (&v)[RT], int rows) {
     constexpr int DP = 64 / G;
-    const int w = threadIdx.x % DP, g = threadIdx.x / DP;
+    const int w = lane_id() % DP, g = lane_id() / DP;
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
         const int row = G * t + g;
@@ -431,7 +435,7 @@ template <int G, int RT>
 __device__ __forceinline__ void load_fwd(const Mat &M, const uint32_t *tab, const uint8_t *H, int pc, int r, int k,
                                          FwdOps<G, RT> &f) {
     constexpr int DP = 64 / G;
-    const int w = threadIdx.x % DP, g = threadIdx.x / DP;
+    const int w = lane_id() % DP, g = lane_id() / DP;
     const uint8_t *h = H + pc * k;
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
@@ -479,11 +483,11 @@ __device__ __forceinline__ uint32_t dot_chunked(const uint32_t *tab, const uint3
 // Runs pieces pc, pc+1, ... on the registers while the matrix stays a clean RREF (the next piece's forward
 // operands are loaded while the current one finishes).  Returns the next piece index; on leaving the clean
 // state (a kept row with a zero diagonal) the whole matrix is written back to LDS and *clean = false.
-template <int G, int RT>
+template <int G, int RT, bool WG = true>
 __device__ int reg_run(const Mat &M, const uint32_t *tab, uint32_t (&v)[RT], const uint8_t *H, int pc, int m, int k,
                        int &rows, bool &clean, int32_t *St PROF_ARGS) {
     constexpr int DP = 64 / G;
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int w = lane % DP, g = lane / DP;
     const bool wl = w < M.D;
     uint32_t cm = 0;  // coefficient bytes (< k) of this lane's dword
@@ -515,9 +519,9 @@ __device__ int reg_run(const Mat &M, const uint32_t *tab, uint32_t (&v)[RT], con
             const bool keep = ballot((nr & cm) != 0) != 0;  // remove_zero_rows (:222-244)
             if (lane == 0) St[pc] = keep ? RLNC_OK : RLNC_ERR_PIECE_NOT_USEFUL;
             if (keep) {  // the row survives with a zero diagonal: leave the clean state (generic path)
-                regs_to_lds<G, RT>(M, v, r);
+                regs_to_lds<G, RT, WG>(M, v, r);
                 if (g == 0 && wl) M.w[r * M.D + w] = nr;
-                __syncthreads();
+                rsync<WG>();
                 rows = r + 1;
                 clean = false;
                 return pc + 1;
@@ -855,6 +859,117 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, in
 #endif
 }
 
+
+// Many small objects (row <= 16 dwords, k <= 16): NW objects per workgroup, one per wave, over ONE LDS copy of the
+// multiplier table.  The one-wave kernel above copies the 16 KiB table per object, which caps a CU at 8 resident
+// objects; here a workgroup of 4 holds 4 objects in ~20 KiB, so all 16 objects per CU of a 4,096-object batch are
+// resident at once.  Per wave the same steps as gf_rref_batch_kernel<4, 8, 1> (register clean run, the reference's
+// rref verbatim when the clean state ends), with wave-local synchronisation only: after the table copy no wave
+// waits for another.
+__host__ __device__ inline size_t rref_small_wave_bytes(int k, int m) {
+    return size_t(k + 1) * 4 * size_t(rref_row_dwords(k, m)) + 4 * ((size_t(m) + 3) & ~size_t(3)) +
+           ((size_t(m) * k + 15) & ~size_t(15));
+}
+constexpr int kSmallNW = 4;
+constexpr int kSmallMinObjects = 2048;
+
+template <int NW, int G, int RT>
+__global__ __launch_bounds__(64 * NW) void gf_rref_small_kernel(RrefParams p) {
+    extern __shared__ uint32_t lds[];
+    uint32_t *tab = lds;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+#ifdef RLNC_RREF_PROFILE  // diagnostic build: statuses 0-3 = reg_run phase cycles, 5 = setup cycles, 6 = entry to
+    // outputs in shader cycles, 7 = the same in 10 ns ticks; rank = the entry tick (100 MHz) of the wave
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    {  // the shared table copy, all loads in flight at once
+        constexpr int kPer = kTabEntries * kTabDw / 4 / (64 * NW);
+        const uint4 *src = reinterpret_cast<const uint4 *>(kRrefTable.v);
+        uint4 *dst = reinterpret_cast<uint4 *>(tab);
+        uint4 t4[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) t4[u] = src[tid + 64 * NW * u];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) dst[tid + 64 * NW * u] = t4[u];
+    }
+    __syncthreads();  // the only workgroup barrier
+    const int o = blockIdx.x * NW + wave;
+    if (o >= p.n_obj) return;
+    const int k = p.k, m = p.m;
+    Mat M;
+    M.D = rref_row_dwords(k, m);
+    M.S = 4 * M.D;
+    M.w = lds + kTabEntries * kTabDw + size_t(wave) * (rref_small_wave_bytes(k, m) / 4);
+    M.b = reinterpret_cast<uint8_t *>(M.w);
+    int32_t *St = reinterpret_cast<int32_t *>(M.b + size_t(k + 1) * M.S);
+    uint8_t *H = reinterpret_cast<uint8_t *>(St + ((m + 3) & ~3));
+    const uint8_t *base = p.pieces + int64_t(o) * p.obj_stride;
+    for (int e0 = 0; e0 < m * k; e0 += 64 * 16) {  // staged headers, 16 byte loads in flight per lane
+        uint8_t hb[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = e0 + lane + 64 * u;
+            hb[u] = e < m * k ? base[int64_t(e / k) * p.piece_stride + e % k] : uint8_t(0);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            if (e0 + lane + 64 * u < m * k) H[e0 + lane + 64 * u] = hb[u];
+    }
+    for (int w = lane; w < (k + 1) * M.D; w += 64) M.w[w] = 0;
+    rsync<false>();
+
+    int rows = 0;
+    bool clean = true;
+    uint32_t v[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) v[t] = 0;
+#ifdef RLNC_RREF_PROFILE
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t prof_t = __builtin_amdgcn_s_memtime();
+    prof[5] = prof_t - t_start;
+#endif
+    for (int pc = 0; pc < m; ++pc) {
+        if (clean) {
+            pc = reg_run<G, RT, false>(M, tab, v, H, pc, m, k, rows, clean, St PROF_PASS);
+            rsync<false>();
+            if (pc >= m) break;
+        }
+        if (rows == k) {  // decoder.rs:97-99
+            if (lane == 0) St[pc] = RLNC_ERR_RECEIVED_ALL_PIECES;
+            continue;
+        }
+        // add_row (decoder_matrix.rs:53-62), then the reference's rref verbatim (decoder_matrix.rs:99-244)
+        for (int c = lane; c < M.S; c += 64) M.b[rows * M.S + c] = c < k ? H[pc * k + c] : uint8_t(c == k + pc);
+        rsync<false>();
+        const int before = rows;
+        rows = generic_rref<false>(M, tab, rows + 1, k);
+        clean = is_clean(M, rows);
+        if (clean) lds_to_regs<G, RT>(M, v, rows);
+        if (lane == 0) St[pc] = rows == before ? RLNC_ERR_PIECE_NOT_USEFUL : RLNC_OK;  // decoder.rs:112-117
+        rsync<false>();
+    }
+    if (clean) regs_to_lds<G, RT, false>(M, v, rows);
+    rsync<false>();
+#ifdef RLNC_RREF_PROFILE
+    prof[6] = __builtin_amdgcn_s_memtime() - t_start;
+    prof[7] = __builtin_amdgcn_s_memrealtime() - rt_start;
+    if (lane == 0)
+        for (int i = 0; i < 8 && i < m; ++i) St[i] = int32_t(prof[i]);
+    rsync<false>();
+#endif
+    for (int pc = lane; pc < m; pc += 64) p.status[int64_t(o) * m + pc] = St[pc];
+#ifdef RLNC_RREF_PROFILE
+    if (lane == 0) p.rank[o] = int32_t(rt_start & 0x7FFFFFFFu);
+#else
+    if (lane == 0) p.rank[o] = rows;
+#endif
+    uint8_t *T = p.T + int64_t(o) * p.T_obj;
+    for (int e = lane; e < k * m; e += 64) {
+        const int r = e / m, s = e % m;
+        T[e] = r < rows ? M.b[r * M.S + k + s] : uint8_t(0);
+    }
+}
 
 // ---------------------------------------------------------------------------------------------------
 // Blocked clean run (path 5, default when k + m <= 256): while rows 0..r-1 are a clean RREF, the next b <= B
@@ -1459,7 +1574,15 @@ static hipError_t launch_rref_one(const RrefParams &p, hipStream_t s) {
     // beats the 4-wave blocked run, whose per-object parallelism the full grid no longer needs -- 4,096 x k = 16:
     // 0.093 vs 0.125 ms, k = 8: 0.051 vs 0.067, k = 16 sparse + dependent: 0.195 vs 0.295; at 512 objects the
     // blocked run stays faster (0.035 vs 0.049) (profiles/r02_elim_small_k.jsonl)
-    const bool small_many = p.lds_only == 0 && p.k <= 16 && p.n_obj >= 2048 && rref_row_dwords(p.k, p.m) <= 16 &&
+#ifdef RLNC_AB_VARIANTS  // A/B knob (read once): RLNC_SMALL_MIN = the object count from which small_many applies
+    static const int small_min = [] {
+        const char *e = getenv("RLNC_SMALL_MIN");
+        return e ? atoi(e) : kSmallMinObjects;
+    }();
+#else
+    constexpr int small_min = kSmallMinObjects;
+#endif
+    const bool small_many = p.lds_only == 0 && p.k <= 16 && p.n_obj >= small_min && rref_row_dwords(p.k, p.m) <= 16 &&
                             rref_lds_bytes_staged(p.k, p.m) <= kRrefMaxLds;
     // the blocked clean run (4 waves per object, the default) when the row fits one wave (k + m <= 256)
     if (!small_many && (p.lds_only == 0 || p.lds_only == 3) && rref_row_dwords(p.k, p.m) <= 64 &&
@@ -1498,6 +1621,31 @@ static hipError_t launch_rref_one(const RrefParams &p, hipStream_t s) {
             }
         }
         hipLaunchKernelGGL(kern, dim3(p.n_obj), dim3(64 * kBlkNW), rref_block_lds_bytes(p.k, p.m), s, p);
+        return hipGetLastError();
+    }
+    if (small_many && p.k <= 16 && rref_row_dwords(p.k, p.m) <= 16) {
+        // kSmallNW objects per workgroup over one table copy (<= 16 KiB + 4 x 2 KiB: under the default LDS limit)
+        // rows of 8 dwords or fewer (k + m <= 32): 8 lane groups of 4 registers (123 VGPRs: 4 waves per SIMD) and
+        // kSmallNW objects per workgroup; wider rows: 4 groups of 8 (199 VGPRs, 2 waves per SIMD, where the 8 objects
+        // per CU the one-object workgroups already hold are all the VGPRs allow) -- profiles/r03_small_elim_ab.txt
+        const bool g8 = rref_row_dwords(p.k, p.m) <= 8;
+        auto kern = g8 ? &gf_rref_small_kernel<kSmallNW, 8, 4> : &gf_rref_small_kernel<1, 4, 8>;
+        int nw = g8 ? kSmallNW : 1;
+#ifdef RLNC_AB_VARIANTS  // A/B knob (read once): RLNC_SMALL_NW = 1, 2, 4 or 8 objects per workgroup
+        static const int nw_ab = [] {
+            const char *e = getenv("RLNC_SMALL_NW");
+            return e ? atoi(e) : kSmallNW;
+        }();
+        if (nw_ab == 1 || nw_ab == 2 || nw_ab == 8) {
+            nw = nw_ab;
+            if (g8)
+                kern = nw == 1 ? &gf_rref_small_kernel<1, 8, 4> : nw == 2 ? &gf_rref_small_kernel<2, 8, 4> : &gf_rref_small_kernel<8, 8, 4>;
+            else
+                kern = nw == 1 ? &gf_rref_small_kernel<1, 4, 8> : nw == 2 ? &gf_rref_small_kernel<2, 4, 8> : &gf_rref_small_kernel<8, 4, 8>;
+        }
+#endif
+        const size_t lds_small = size_t(kTabEntries) * kTabDw * 4 + nw * rref_small_wave_bytes(p.k, p.m);
+        hipLaunchKernelGGL(kern, dim3((p.n_obj + nw - 1) / nw), dim3(64 * nw), lds_small, s, p);
         return hipGetLastError();
     }
     size_t lds = rref_lds_bytes(p.k, p.m);

@@ -790,14 +790,16 @@ def test_large_piece_count_recode(ctx, orc, k, n, count):
         assert np.array_equal(got[c], orc.recode(pieces, k + L, k, r[0, c])), c
 
 
-@pytest.mark.parametrize("k,m,sparsity,dep", [(16, 16, 0.0, 0.0), (16, 24, 0.5, 0.1), (8, 12, 0.7, 0.1)])
-def test_decode_many_small_objects(ctx, k, m, sparsity, dep):
-    """2,048 objects with k <= 16: the default path takes the one-wave register kernel (rref.hip `small_many`);
-    every object's statuses and payload rows against the oracle."""
+@pytest.mark.parametrize("k,m,sparsity,dep,nobj", [(16, 16, 0.0, 0.0, 2048), (16, 24, 0.5, 0.1, 2051),
+                                                  (8, 12, 0.7, 0.1, 2049)])
+def test_decode_many_small_objects(ctx, k, m, sparsity, dep, nobj):
+    """>= 2,048 objects with k <= 16: the default path takes the multi-object kernel (rref.hip gf_rref_small_kernel,
+    4 objects per workgroup: 2,049 and 2,051 leave the last workgroup part-empty; rows of <= 8 dwords on 8 lane
+    groups, else 4); every object's statuses and payload rows against the oracle."""
     from rlnc_amd import batch
 
     rng = np.random.default_rng(2048 + k * 3 + m)
-    nobj, L = 2048, 8
+    L = 8
     seqs = _sequences(rng, nobj, k, m, L, sparsity, dep)
     decoded = dev(np.zeros((nobj, k, L), np.uint8))
     pst, ost, dl = batch.decode_batch(dev(seqs), k, decoded, ctx)
