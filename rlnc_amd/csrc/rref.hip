@@ -117,6 +117,10 @@ __device__ __forceinline__ uint32_t mul4(const uint32_t *tab, uint32_t q, uint32
     return __builtin_amdgcn_perm(t.y, t.x, x & 0x07070707u) ^ __builtin_amdgcn_perm(t.w, t.z, (x >> 3) & 0x07070707u) ^
            __builtin_amdgcn_perm(t2, t2, (x >> 6) & 0x03030303u);
 }
+__device__ __forceinline__ uint32_t mul4t(uint4 t, uint32_t t2, uint32_t x) {
+    return __builtin_amdgcn_perm(t.y, t.x, x & 0x07070707u) ^ __builtin_amdgcn_perm(t.w, t.z, (x >> 3) & 0x07070707u) ^
+           __builtin_amdgcn_perm(t2, t2, (x >> 6) & 0x03030303u);
+}
 __device__ __forceinline__ uint32_t gfmul(const uint32_t *tab, uint32_t a, uint32_t b) {
     return mul4(tab, a, b) & 0xFFu;
 }
@@ -164,6 +168,60 @@ __device__ __forceinline__ void rsync() {
     }
 }
 
+// Rows j in [j_lo, j_hi) with M[j][i] != 0: row_j[c >= i] ^= (M[j][i] / M[i][i])·row_i[c >= i] -- the bodies of the
+// reference's per-row loops (decoder_matrix.rs:143-162 forward, :179-198 backward).  They are independent across j
+// (each reads row i, which the step leaves unchanged, and writes its own row), so rows under 64 dwords go 64 / D rows
+// per pass, lane = (row, dword), with the quotient byte read before the same instruction stream rewrites it; wider
+// rows one at a time over the lanes, the nonzero rows found by ballot.
+__device__ __forceinline__ void eliminate_rows(const Mat &M, const uint32_t *tab, int i, uint32_t inv, int j_lo,
+                                               int j_hi) {
+    const int lane = lane_id();
+    const int D = M.D;
+    if (D < 64) {
+        const int RP = 64 / D, w = lane % D, jr = lane / D;
+        const uint32_t mask = from_mask(w, i);
+        const uint32_t xi = M.w[i * D + w];
+        const uint4 ti4 = *reinterpret_cast<const uint4 *>(tab + inv * kTabDw);  // the quotient = c · inv
+        const uint32_t ti2 = tab[inv * kTabDw + 4];
+        if (j_hi - j_lo <= 2 * RP) {  // at most two passes over the range: no compaction (one LDS round trip less)
+            for (int j0 = j_lo; j0 < j_hi; j0 += RP) {
+                const int j = j0 + jr;
+                if (j < j_hi) {
+                    const uint32_t c = M.at(j, i);
+                    if (c != 0u) M.w[j * D + w] ^= mul4(tab, mul4t(ti4, ti2, c) & 0xFFu, xi) & mask;  // :148 / :184
+                }
+            }
+            return;
+        }
+        for (int g = j_lo; g < j_hi; g += 64) {
+            const int jl = g + lane;
+            uint64_t b = ballot(jl < j_hi && M.at(jl, i) != 0);  // the rows with work, 64 at a time
+            while (b) {  // RP of them per pass: lane group jr takes the jr-th remaining set bit
+                uint64_t bb = b;
+                for (int t = 0; t < RP - 1; ++t)
+                    if (t < jr) bb &= bb - 1;
+                if (bb) {
+                    const int j = g + __ffsll((unsigned long long)bb) - 1;
+                    const uint32_t q = mul4t(ti4, ti2, M.at(j, i)) & 0xFFu;  // :148 / :184
+                    M.w[j * D + w] ^= mul4(tab, q, xi) & mask;
+                }
+                for (int t = 0; t < RP && b; ++t) b &= b - 1;
+            }
+        }
+        return;
+    }
+    for (int g = j_lo; g < j_hi; g += 64) {
+        const int j = g + lane;
+        uint64_t b = ballot(j < j_hi && M.at(j, i) != 0);
+        while (b) {
+            const int jj = g + __ffsll((unsigned long long)b) - 1;
+            b &= b - 1;
+            const uint32_t q = gfmul(tab, M.at(jj, i), inv);  // :148 / :184
+            row_muladd(M, tab, jj, i, q, i);
+        }
+    }
+}
+
 // DecoderMatrix::rref — decoder_matrix.rs:99-244, verbatim.  Returns the new row count.
 template <bool WG = true>
 __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
@@ -188,16 +246,7 @@ __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
             piv = M.at(i, i);
         }
         const uint32_t inv = gfinv(tab, piv);
-        for (int g = i + 1; g < R; g += 64) {
-            const int j = g + lane;
-            uint64_t b = ballot(j < R && M.at(j, i) != 0);
-            while (b) {
-                const int jj = g + __ffsll((unsigned long long)b) - 1;
-                b &= b - 1;
-                const uint32_t q = gfmul(tab, M.at(jj, i), inv);  // :148
-                row_muladd(M, tab, jj, i, q, i);
-            }
-        }
+        eliminate_rows(M, tab, i, inv, i + 1, R);
         rsync<WG>();
     }
     // clean_backward :171-215
@@ -205,16 +254,7 @@ __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
         const uint32_t piv = M.at(i, i);
         if (piv == 0) continue;
         const uint32_t inv = gfinv(tab, piv);
-        for (int g = 0; g < i; g += 64) {
-            const int j = g + lane;
-            uint64_t b = ballot(j < i && M.at(j, i) != 0);
-            while (b) {
-                const int jj = g + __ffsll((unsigned long long)b) - 1;
-                b &= b - 1;
-                const uint32_t q = gfmul(tab, M.at(jj, i), inv);  // :184
-                row_muladd(M, tab, jj, i, q, i);
-            }
-        }
+        eliminate_rows(M, tab, i, inv, 0, i);
         rsync<WG>();
         if (piv != 1) {  // :200-211
             for (int w = lane; w < M.D; w += 64) {
@@ -254,6 +294,39 @@ __device__ int generic_rref(const Mat &M, const uint32_t *tab, int R, int k) {
     return dst;
 }
 
+// XOR over the G lane groups (lane blocks of DP = 64 / G): a DPP row rotation below 16 lanes, then the gfx950
+// permlane swaps across rows and half-waves -- VALU only (__shfl_xor costs one dependent ds_bpermute per step)
+template <int DP>
+__device__ __forceinline__ uint32_t group_xor(uint32_t a) {
+    // inside a 16-lane row: rotations by 8, 4, 2, 1 down to DP (each lane ends with the XOR of its residue class)
+    if constexpr (DP <= 1) a ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x121, 0xf, 0xf, false));  // row_ror:1
+    if constexpr (DP <= 2) a ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x122, 0xf, 0xf, false));  // row_ror:2
+    if constexpr (DP <= 4) a ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x124, 0xf, 0xf, false));  // row_ror:4
+    if constexpr (DP <= 8) a ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x128, 0xf, 0xf, false));  // row_ror:8
+    if constexpr (DP <= 16) {  // odd rows of one operand swap with even rows of the other: x ^ x[lane ^ 16]
+        const auto s = __builtin_amdgcn_permlane16_swap(a, a, false, false);
+        a = s[0] ^ s[1];
+    }
+    if constexpr (DP <= 32) {  // upper half-wave of one operand swaps with the lower of the other: x ^ x[lane ^ 32]
+        const auto s = __builtin_amdgcn_permlane32_swap(a, a, false, false);
+        a = s[0] ^ s[1];
+    }
+    return a;
+}
+
+// the same for a run-time group width D (a power of two; D >= 64: one group, nothing to reduce)
+__device__ __forceinline__ uint32_t group_xor_rt(uint32_t a, int D) {
+    switch (D) {
+        case 1: return group_xor<1>(a);
+        case 2: return group_xor<2>(a);
+        case 4: return group_xor<4>(a);
+        case 8: return group_xor<8>(a);
+        case 16: return group_xor<16>(a);
+        case 32: return group_xor<32>(a);
+        default: return a;
+    }
+}
+
 // rows 0..R-1 a clean RREF: M[i][i] = 1 and column i zero in every other row (i < R)
 __device__ bool is_clean(const Mat &M, int R) {
     const int lane = lane_id();
@@ -261,7 +334,13 @@ __device__ bool is_clean(const Mat &M, int R) {
     for (int g = 0; g < R; g += 64) {
         const int j = g + lane;
         if (j < R)
-            for (int i = 0; i < R && ok; ++i) ok = M.at(j, i) == (i == j ? 1u : 0u);
+            for (int c4 = 0; 4 * c4 < R; ++c4) {  // bytes 0..R-1 of row j a dword at a time (no early exit: the
+                // reads issue together)
+                const uint32_t x = M.w[j * M.D + c4];
+                const uint32_t want = (j >> 2) == c4 ? 1u << (8 * (j & 3)) : 0u;
+                const uint32_t mask = 4 * c4 + 4 <= R ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (8 * (4 * c4 + 4 - R)));
+                ok = ok && ((x ^ want) & mask) == 0u;
+            }
     }
     return ballot(!ok) == 0;
 }
@@ -315,7 +394,7 @@ __device__ int clean_append(const Mat &M, const uint32_t *tab, int r, int k, boo
             for (int u = 0; u < kU; ++u) acc ^= mul4(tab, q[u], x[u]);
         }
         if (D < 64) {  // reduce the G partial sums (groups are lane blocks of D)
-            for (int sh = D; sh < 64; sh <<= 1) acc ^= __shfl_xor(acc, sh);
+            acc = group_xor_rt(acc, D);
         }
         if (g == 0 && ww < D) M.w[r * D + ww] ^= acc;
         __syncthreads();
@@ -414,10 +493,6 @@ __device__ void lds_to_regs(const Mat &M, uint32_t (&v)[RT], int rows) {
     }
 }
 
-__device__ __forceinline__ uint32_t mul4t(uint4 t, uint32_t t2, uint32_t x) {
-    return __builtin_amdgcn_perm(t.y, t.x, x & 0x07070707u) ^ __builtin_amdgcn_perm(t.w, t.z, (x >> 3) & 0x07070707u) ^
-           __builtin_amdgcn_perm(t2, t2, (x >> 6) & 0x03030303u);
-}
 
 // Forward operands of one piece for the current row count r: this lane's dword of the initial row
 // [coeffs | unit vector of slot pc] and its quotients M[r][i] = coefficient i (i = G·t + g < r); with few
@@ -438,9 +513,10 @@ __device__ __forceinline__ void load_fwd(const Mat &M, const uint32_t *tab, cons
     const int w = lane_id() % DP, g = lane_id() / DP;
     const uint8_t *h = H + pc * k;
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
+    for (int t = 0; t < RT; ++t) {  // unconditional (clamped) reads: all in flight at once, then selected
         const int i = G * t + g;
-        f.q[t] = i < r ? uint32_t(h[i]) : 0u;
+        const uint32_t x = h[i < k ? i : k - 1];
+        f.q[t] = i < r ? x : 0u;
     }
     uint32_t init = 0;
     if (w < M.D) {
@@ -509,8 +585,7 @@ __device__ int reg_run(const Mat &M, const uint32_t *tab, uint32_t (&v)[RT], con
         } else {
             acc = dot_chunked<RT>(tab, f.q, v);
         }
-#pragma unroll
-        for (int sh = DP; sh < 64; sh <<= 1) acc ^= __shfl_xor(acc, sh);
+        acc = group_xor<DP>(acc);
         uint32_t nr = f.init ^ acc;
         PROF_MARK(2);
         const int rw = r >> 2, rb = 8 * (r & 3);
@@ -629,8 +704,7 @@ __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, u
         } else {
             acc = dot_chunked<RTW>(tab, q, v);
         }
-#pragma unroll
-        for (int sh = DP; sh < 64; sh <<= 1) acc ^= __shfl_xor(acc, sh);
+        acc = group_xor<DP>(acc);
         uint32_t *Pb = P + buf * NW * DP;
         if (lane < DP) Pb[wave * DP + lane] = acc;
         PROF_MARK(2);
@@ -874,7 +948,7 @@ constexpr int kSmallNW = 4;
 constexpr int kSmallMinObjects = 2048;
 
 template <int NW, int G, int RT>
-__global__ __launch_bounds__(64 * NW) void gf_rref_small_kernel(RrefParams p) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 ? 4 : 1))) void gf_rref_small_kernel(RrefParams p) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1213,7 +1287,7 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
                     for (int t = 0; t < B; ++t) {
                         if (t < nb) {
                             uint32_t a = acc[t];
-                            for (int sh = D; sh < 64; sh <<= 1) a ^= __shfl_xor(a, sh);
+                            a = group_xor_rt(a, D);
                             if (g == 0 && a) atomicXor(&X[t * D + w], a);
                         }
                     }
@@ -1339,7 +1413,7 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
             for (int t = 0; t < B; ++t) {
                 if (t < b) {
                     uint32_t a = acc[t];
-                    for (int sh = D; sh < 64; sh <<= 1) a ^= __shfl_xor(a, sh);
+                    a = group_xor_rt(a, D);
                     if (g == 0 && a) atomicXor(&X[t * D + w], a);
                 }
             }

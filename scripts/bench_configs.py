@@ -78,31 +78,38 @@ def main():
                 "roundtrip_GiBps": round((enc_b + dec_b) / (t_enc + t_dec) / 1e-3 / GIB, 1),
                 "full_rank_objects": int(full_rank.sum()), "verified": ok}
 
+    def recode(out):  # configs[3]: recoder over 64 coded pieces (k = 64, L = 256 KiB) -> 64 recoded pieces
+        B, k, L, n, cnt = 16, 64, 1 << 18, 64, 64
+        src, co, r = rnd(B, k, L), rnd(B, n, k), rnd(B, cnt, n)
+        pieces = torch.empty((B, n, k + L), dtype=torch.uint8, device=dev)
+        batch.encode_batch(src, co, pieces, ctx)
+        rec = torch.empty((B, cnt, k + L), dtype=torch.uint8, device=dev)
+        t_rec = timed(lambda: batch.recode_batch(pieces, r, rec, k, ctx), rounds)
+        dec = torch.empty((B, k, L), dtype=torch.uint8, device=dev)
+        pst = torch.empty((B, cnt), dtype=torch.int32, device=dev)
+        ost = torch.empty((B,), dtype=torch.int32, device=dev)
+        dl = torch.empty((B,), dtype=torch.int64, device=dev)
+        batch.decode_batch_device(rec, k, dec, pst, ost, dl, ctx)
+        torch.cuda.synchronize()
+        fr = (pst == 0).sum(1) == k
+        rec_b = B * cnt * (n + 1) * (k + L)
+        out.append({"config": "configs[3] recode", "objects": B, "k": k, "piece_bytes": L, "received": n,
+                    "recoded": cnt, "recode_ms": round(t_rec, 4),
+                    "recode_GiBps": round(rec_b / t_rec / 1e-3 / GIB, 1),
+                    "recode_T_muladd_per_s": round(B * cnt * n * (k + L) / t_rec / 1e9, 2),
+                    "verified": bool(torch.equal(dec[fr], src[fr])) and bool(fr.any())})
+
+    only = os.environ.get("CONFIGS")  # a subset, e.g. CONFIGS=0 or CONFIGS=1,3 (profiling runs)
+    want = (lambda c: only is None or c in only.split(","))
     out = []
-    out.append(enc_dec("configs[1]+[2] (bench)", 16, 32, 1 << 20, 64, 32))
-    # configs[3]: recoder over 64 coded pieces (k = 64, L = 256 KiB) -> 64 recoded pieces
-    B, k, L, n, cnt = 16, 64, 1 << 18, 64, 64
-    src, co, r = rnd(B, k, L), rnd(B, n, k), rnd(B, cnt, n)
-    pieces = torch.empty((B, n, k + L), dtype=torch.uint8, device=dev)
-    batch.encode_batch(src, co, pieces, ctx)
-    rec = torch.empty((B, cnt, k + L), dtype=torch.uint8, device=dev)
-    t_rec = timed(lambda: batch.recode_batch(pieces, r, rec, k, ctx), rounds)
-    dec = torch.empty((B, k, L), dtype=torch.uint8, device=dev)
-    pst = torch.empty((B, cnt), dtype=torch.int32, device=dev)
-    ost = torch.empty((B,), dtype=torch.int32, device=dev)
-    dl = torch.empty((B,), dtype=torch.int64, device=dev)
-    batch.decode_batch_device(rec, k, dec, pst, ost, dl, ctx)
-    torch.cuda.synchronize()
-    fr = (pst == 0).sum(1) == k
-    rec_b = B * cnt * (n + 1) * (k + L)
-    out.append({"config": "configs[3] recode", "objects": B, "k": k, "piece_bytes": L, "received": n,
-                "recoded": cnt, "recode_ms": round(t_rec, 4),
-                "recode_GiBps": round(rec_b / t_rec / 1e-3 / GIB, 1),
-                "recode_T_muladd_per_s": round(B * cnt * n * (k + L) / t_rec / 1e9, 2),
-                "verified": bool(torch.equal(dec[fr], src[fr])) and bool(fr.any())})
-    del src, co, r, pieces, rec, dec
-    out.append(enc_dec("configs[4] batch (512 of 4096 objects per GPU)", 512, 128, 1 << 16, 128, 128))
-    out.append(enc_dec("configs[0] shape at device scale", 4096, 16, 4096, 16, 16))
+    if want("1"):
+        out.append(enc_dec("configs[1]+[2] (bench)", 16, 32, 1 << 20, 64, 32))
+    if want("3"):
+        recode(out)
+    if want("4"):
+        out.append(enc_dec("configs[4] batch (512 of 4096 objects per GPU)", 512, 128, 1 << 16, 128, 128))
+    if want("0"):
+        out.append(enc_dec("configs[0] shape at device scale", 4096, 16, 4096, 16, 16))
     for line in out:
         print(json.dumps(line), flush=True)
 
