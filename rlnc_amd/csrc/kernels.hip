@@ -1623,12 +1623,128 @@ hipError_t launch_final_data_len_ranked(const uint8_t *data, int64_t obj_stride,
     return hipGetLastError();
 }
 
-static bool matmul_aligned(const MatmulParams &p) {
-    return al16(p.in) && al16(p.out) && al16(p.in_row) && al16(p.out_row) &&
-           (p.n_obj == 1 || (al16(p.in_obj) && al16(p.out_obj)));
+// 16-byte alignment of an operand: its base, and the strides of the dimensions that have more than one element (a
+// single row's stride is never used)
+static bool in_aligned(const MatmulParams &p) {
+    return al16(p.in) && (p.n_in == 1 || al16(p.in_row)) && (p.n_obj == 1 || al16(p.in_obj));
+}
+static bool out_aligned(const MatmulParams &p) {
+    return al16(p.out) && (p.n_out == 1 || al16(p.out_row)) && (p.n_obj == 1 || al16(p.out_obj));
+}
+static bool matmul_aligned(const MatmulParams &p) { return in_aligned(p) && out_aligned(p); }
+
+// ---------------------------------------------------------------------------------------------------
+// Realigned products.  A piece row is rarely 16-byte aligned: Encoder::new pads to L = ceil((len + 1) / k)
+// (encoder.rs:93-95), so the reference's own bench shapes (2^20..2^25 bytes over k = 16..256) give odd L, and a
+// coded piece's data starts at byte k of a (k + L)-byte row.  The vector kernels need 16-byte rows; the byte-granular
+// kernels run 5-7x slower.  So a misaligned operand of a product the bit-sliced or stream kernels take is copied
+// into 16-byte-aligned scratch rows (input) or out of them (output) around the aligned product, in chunks of objects
+// and column blocks of at most kRealignBudget bytes of scratch.
+// ---------------------------------------------------------------------------------------------------
+constexpr size_t kRealignBudget = size_t(512) << 20;
+constexpr int kRealignDwords = 4;  // destination dwords per thread
+
+// dst[o][r][0:w) = src[o][r][0:w) at any byte alignment of either side: thread t writes dwords of the destination's
+// 4-byte grid (a dword the row covers only in part is written byte by byte, so the neighbouring bytes -- e.g. the
+// coded piece's coefficient header -- are never touched), reading the source as aligned dwords joined by v_alignbyte;
+// every dword read holds at least one byte of the row, so no read leaves the row's pages
+__global__ __launch_bounds__(256) void realign_rows_kernel(uint8_t *dst, int64_t dst_row, int64_t dst_obj,
+                                                           const uint8_t *src, int64_t src_row, int64_t src_obj,
+                                                           int rows, int64_t width, int chunks) {
+    const int64_t wg = blockIdx.x;
+    const int64_t rr = wg / chunks;
+    const int64_t ch = wg % chunks;
+    const int64_t o = rr / rows, r = rr % rows;
+    uint8_t *d = dst + o * dst_obj + r * dst_row;
+    const uint8_t *sp = src + o * src_obj + r * src_row;
+    const int dmis = int(reinterpret_cast<uintptr_t>(d) & 3);
+    uint32_t *dw = reinterpret_cast<uint32_t *>(d - dmis);
+    const int64_t ndw = (dmis + width + 3) >> 2;  // dword t covers row bytes [4t - dmis, 4t - dmis + 4)
+#pragma unroll
+    for (int u = 0; u < kRealignDwords; ++u) {
+        const int64_t t = ch * (256 * kRealignDwords) + u * 256 + threadIdx.x;
+        if (t >= ndw) break;
+        const int64_t x0 = 4 * t - dmis;
+        if (x0 >= 0 && x0 + 4 <= width) {
+            const uintptr_t a = reinterpret_cast<uintptr_t>(sp + x0);
+            const uint32_t *A = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+            const uint32_t sh = uint32_t(a & 3);
+            const uint32_t lo = A[0];
+            const uint32_t hi = sh ? A[1] : 0u;
+            dw[t] = __builtin_amdgcn_alignbyte(hi, lo, sh);  // ({hi, lo} >> 8 sh)[31:0]
+        } else {
+            for (int b = 0; b < 4; ++b) {
+                const int64_t x = x0 + b;
+                if (x >= 0 && x < width) d[x] = sp[x];
+            }
+        }
+    }
+}
+
+static hipError_t launch_realign(uint8_t *dst, int64_t dst_row, int64_t dst_obj, const uint8_t *src, int64_t src_row,
+                                 int64_t src_obj, int rows, int64_t width, int n_obj, hipStream_t s) {
+    const int64_t per_wg = 256 * kRealignDwords * 4;
+    const int64_t chunks = (width + 3 + per_wg) / per_wg;  // dwords of the destination grid, + 1 for its offset
+    const int64_t total = int64_t(n_obj) * rows * chunks;
+    if (total <= 0) return hipSuccess;
+    if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(realign_rows_kernel, dim3(unsigned(total)), dim3(256), 0, s, dst, dst_row, dst_obj, src, src_row,
+                       src_obj, rows, width, int(chunks));
+    return hipGetLastError();
+}
+
+static bool jump_variant(MatmulVariant v) {
+    return v == MatmulVariant::BitSlicedJump || v == MatmulVariant::BitSlicedJumpShared ||
+           v == MatmulVariant::BitSlicedJumpShared8 || v == MatmulVariant::BitSlicedJumpRun;
+}
+
+struct RealignPlan {
+    bool in_mis = false, out_mis = false;
+    int objs = 0;                           // objects per chunk
+    int64_t cw = 0;                         // columns per chunk (a multiple of 4 KiB, or the whole width)
+    int64_t lr = 0;                         // scratch row stride (cw rounded up to 16)
+    size_t prod_bytes = 0, in_bytes = 0, out_bytes = 0;
+};
+
+size_t matmul_scratch_bytes_aligned(const MatmulParams &p, MatmulVariant v);
+
+// The realigned form of a misaligned product that the bit-sliced or stream kernels would take if it were aligned
+static bool realign_plan(const MatmulParams &p, MatmulVariant v, RealignPlan &r) {
+    if (!jump_variant(v) || p.width < kColBlock || p.n_out <= 0 || p.n_in <= 0 || p.n_obj <= 0 || matmul_aligned(p))
+        return false;
+    r.in_mis = !in_aligned(p);
+    r.out_mis = !out_aligned(p);
+    const int64_t rows = (r.in_mis ? p.n_in : 0) + (r.out_mis ? p.n_out : 0);
+    const int64_t whole = (p.width + 15) & ~int64_t(15);
+    int64_t objs = p.n_obj, cw = whole;
+    if (objs * rows * cw > int64_t(kRealignBudget)) {
+        cw = std::max<int64_t>(kColBlock, int64_t(kRealignBudget) / (objs * rows) / kColBlock * kColBlock);
+        if (cw >= whole) cw = whole;
+        if (objs * rows * cw > int64_t(kRealignBudget)) objs = std::max<int64_t>(1, int64_t(kRealignBudget) / (rows * cw));
+    }
+    r.objs = int(objs);
+    r.cw = cw;
+    r.lr = (cw + 15) & ~int64_t(15);
+    MatmulParams q = p;  // one chunk, aligned
+    q.n_obj = r.objs;
+    q.width = std::min<int64_t>(cw, p.width);
+    q.in = q.out = nullptr;
+    q.in_row = q.out_row = r.lr;
+    q.in_obj = int64_t(p.n_in) * r.lr;
+    q.out_obj = int64_t(p.n_out) * r.lr;
+    r.prod_bytes = (matmul_scratch_bytes_aligned(q, v) + 255) & ~size_t(255);
+    r.in_bytes = r.in_mis ? size_t(objs) * p.n_in * r.lr : 0;
+    r.out_bytes = r.out_mis ? size_t(objs) * p.n_out * r.lr : 0;
+    return true;
 }
 
 size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v) {
+    RealignPlan r;
+    if (realign_plan(p, v, r)) return r.prod_bytes + r.in_bytes + r.out_bytes;
+    return matmul_scratch_bytes_aligned(p, v);
+}
+
+size_t matmul_scratch_bytes_aligned(const MatmulParams &p, MatmulVariant v) {
     if ((v != MatmulVariant::BitSliced && v != MatmulVariant::BitSlicedJump && v != MatmulVariant::BitSlicedJumpShared &&
          v != MatmulVariant::BitSlicedJumpShared8 && v != MatmulVariant::BitSlicedJumpRun) ||
         p.n_out <= 0 || p.n_in <= 0 || p.n_obj <= 0)
@@ -1647,6 +1763,45 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
     if (p.n_out <= 0 || p.width <= 0 || p.n_obj <= 0) return hipSuccess;
     const bool aligned = matmul_aligned(p);
     if (p.n_in <= 0) return hipErrorInvalidValue;
+    RealignPlan r;
+    if (realign_plan(p, v, r)) {  // misaligned rows: realign copies around the aligned product
+        if (scratch == nullptr || scratch_bytes < r.prod_bytes + r.in_bytes + r.out_bytes) return hipErrorInvalidValue;
+        uint8_t *ib = static_cast<uint8_t *>(scratch) + r.prod_bytes;
+        uint8_t *ob = ib + r.in_bytes;
+        for (int o0 = 0; o0 < p.n_obj; o0 += r.objs) {
+            const int c = std::min(r.objs, p.n_obj - o0);
+            for (int64_t c0 = 0; c0 < p.width; c0 += r.cw) {
+                const int64_t w = std::min(r.cw, p.width - c0);
+                MatmulParams q = p;
+                q.n_obj = c;
+                q.width = w;
+                q.in = p.in + int64_t(o0) * p.in_obj + c0;
+                q.coef = p.coef + int64_t(o0) * p.coef_obj;
+                q.out = p.out + int64_t(o0) * p.out_obj + c0;
+                q.hdr = (p.hdr != nullptr && c0 == 0) ? p.hdr + int64_t(o0) * p.hdr_obj : nullptr;
+                hipError_t e;
+                if (r.in_mis) {
+                    if ((e = launch_realign(ib, r.lr, int64_t(p.n_in) * r.lr, q.in, p.in_row, p.in_obj, p.n_in, w, c, s)) !=
+                        hipSuccess)
+                        return e;
+                    q.in = ib;
+                    q.in_row = r.lr;
+                    q.in_obj = int64_t(p.n_in) * r.lr;
+                }
+                if (r.out_mis) {
+                    q.out = ob;
+                    q.out_row = r.lr;
+                    q.out_obj = int64_t(p.n_out) * r.lr;
+                }
+                if ((e = launch_matmul(q, s, v, scratch, r.prod_bytes)) != hipSuccess) return e;
+                if (r.out_mis &&
+                    (e = launch_realign(p.out + int64_t(o0) * p.out_obj + c0, p.out_row, p.out_obj, ob, r.lr,
+                                        int64_t(p.n_out) * r.lr, p.n_out, w, c, s)) != hipSuccess)
+                    return e;
+            }
+        }
+        return hipSuccess;
+    }
     const bool jump = v == MatmulVariant::BitSlicedJump || v == MatmulVariant::BitSlicedJumpShared ||
                       v == MatmulVariant::BitSlicedJumpShared8 || v == MatmulVariant::BitSlicedJumpRun;
     if (jump && aligned && p.n_out <= 3 && p.width >= kColBlock) {
