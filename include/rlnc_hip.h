@@ -81,6 +81,12 @@ int rlnc_context_use_own_stream(rlnc_context *ctx);
 void *rlnc_context_get_stream(rlnc_context *ctx);
 int rlnc_context_synchronize(rlnc_context *ctx);
 int rlnc_context_device(const rlnc_context *ctx);
+/* 1 when 16-byte vector loads/stores (and LDS-DMA) at any byte address return the right bytes on `device` (the
+ * queue's unaligned memory mode, checked by a probe kernel when the first context on the device is created):
+ * piece rows at any alignment (odd L from Encoder::new, data at byte k of a (k + L)-byte coded piece) then take the
+ * vector kernels directly; 0: misaligned rows are copied through 16-byte-aligned scratch around them (same results).
+ * -1 before a context exists on the device.  RLNC_ASSUME_ALIGNED_ONLY=1 in the environment forces 0. */
+int rlnc_device_unaligned_vector_access(int device);
 
 /* ---- L1: vector primitives on device buffers (src/common/simd/mod.rs) --------------------------------
  * Same scalar early-outs as the reference (0 → zero-fill / no-op, 1 → no-op / plain XOR). */

@@ -192,6 +192,7 @@ int rlnc_context_create(int device, rlnc_context **out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return set_error(RLNC_ERR_NO_DEVICE, "device %d is %s, librlnc_hip is built for gfx950 only", device,
                          prop.gcnArchName);
+    (void)rlnc::probe_unaligned_vector_access(device);  // once per device: rows at any byte alignment on the vector path
     auto *c = new (std::nothrow) rlnc_context;
     if (!c) return set_error(RLNC_ERR_OUT_OF_MEMORY, "context allocation");
     c->device = device;
@@ -224,6 +225,7 @@ int rlnc_context_use_own_stream(rlnc_context *ctx) {
 
 void *rlnc_context_get_stream(rlnc_context *ctx) { return ctx ? ctx->stream : nullptr; }
 int rlnc_context_device(const rlnc_context *ctx) { return ctx ? ctx->device : -1; }
+int rlnc_device_unaligned_vector_access(int device) { return rlnc::unaligned_vector_access(device); }
 
 int rlnc_context_synchronize(rlnc_context *ctx) {
     CHECK_ARG(ctx != nullptr);

@@ -19,8 +19,10 @@
 // north-star's literal design; it is kept as the ablation baseline.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
+#include <vector>
 
 #include "../../include/rlnc_hip.h"
 #include "gf256.hpp"
@@ -1517,7 +1519,7 @@ hipError_t launch_vec(uint8_t *dst, const uint8_t *src, int64_t len, uint8_t c, 
     const PermTable t = make_perm_table(c);
     const int64_t chunks = (len + kBytesPerThread - 1) / kBytesPerThread;
     const int blocks = int(std::min<int64_t>((chunks + kThreads - 1) / kThreads, 2048));
-    const bool aligned = al16(dst) && (OP == 0 || al16(src));
+    const bool aligned = unaligned_vector_ok() || (al16(dst) && (OP == 0 || al16(src)));
     if (aligned)
         hipLaunchKernelGGL((gf_vec_kernel<OP, true>), dim3(blocks), dim3(kThreads), 0, s, dst, src, len, t.t0lo, t.t0hi,
                            t.t1lo, t.t1hi, t.t2);
@@ -1610,7 +1612,7 @@ hipError_t launch_final_data_len_ranked(const uint8_t *data, int64_t obj_stride,
                                         const int32_t *rank, unsigned long long *scratch, int32_t *status,
                                         int64_t *final_len, hipStream_t s) {
     if (n_obj <= 0) return hipSuccess;
-    if (al16(data) && (n_obj == 1 || al16(obj_stride)))
+    if (unaligned_vector_ok() || (al16(data) && (n_obj == 1 || al16(obj_stride))))
         hipLaunchKernelGGL(last_nonzero_kernel<true>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch, rank,
                            k);
     else
@@ -1624,14 +1626,100 @@ hipError_t launch_final_data_len_ranked(const uint8_t *data, int64_t obj_stride,
 }
 
 // 16-byte alignment of an operand: its base, and the strides of the dimensions that have more than one element (a
-// single row's stride is never used)
+// single row's stride is never used).  On a device that executes 16-byte vector memory instructions at any byte
+// address (unaligned_vector_ok) every operand counts as aligned.
 static bool in_aligned(const MatmulParams &p) {
-    return al16(p.in) && (p.n_in == 1 || al16(p.in_row)) && (p.n_obj == 1 || al16(p.in_obj));
+    return unaligned_vector_ok() ||
+           (al16(p.in) && (p.n_in == 1 || al16(p.in_row)) && (p.n_obj == 1 || al16(p.in_obj)));
 }
 static bool out_aligned(const MatmulParams &p) {
-    return al16(p.out) && (p.n_out == 1 || al16(p.out_row)) && (p.n_obj == 1 || al16(p.out_obj));
+    return unaligned_vector_ok() ||
+           (al16(p.out) && (p.n_out == 1 || al16(p.out_row)) && (p.n_obj == 1 || al16(p.out_obj)));
 }
 static bool matmul_aligned(const MatmulParams &p) { return in_aligned(p) && out_aligned(p); }
+
+// ---------------------------------------------------------------------------------------------------
+// Byte-misaligned vector memory access.  gfx9 executes global_load/store_dwordx4 and global_load_lds_dwordx4 at any
+// byte address when the queue's SH_MEM_CONFIG alignment mode is "unaligned" (the ROCm driver's default for compute
+// queues; in "dword" mode the low address bits are dropped).  Measured on the MI355X boxes
+// (scripts/ubench_unaligned.hip, profiles/r03_ubench_unaligned.jsonl): exact bytes at every offset, and a 1 GiB copy
+// at 4.3-5.2 TB/s misaligned against 4.8 aligned.  A probe kernel checks it once per device; where it holds, rows at
+// any alignment take the vector kernels directly, else the realigned path (realign_plan) copies them through
+// 16-byte scratch rows.  RLNC_ASSUME_ALIGNED_ONLY=1 forces the realigned path (its tests).
+// ---------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void unaligned_probe_kernel(const uint8_t *src, uint8_t *dst, uint8_t *dst_lds) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[64 * 4];
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const int l = threadIdx.x;
+    const int off = 1 + l % 15;  // every misalignment 1..15
+    const uint8_t *s = src + 32 * l + off;
+    uint8_t *d = dst + 32 * l + (16 - off);
+    u4 x;
+    asm volatile("global_load_dwordx4 %0, %1, off\n s_waitcnt vmcnt(0)" : "=v"(x) : "v"(s) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off\n s_waitcnt vmcnt(0)" ::"v"(d), "v"(x) : "memory");
+    __builtin_amdgcn_global_load_lds(s, (__attribute__((address_space(3))) void *)buf, 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    reinterpret_cast<u4 *>(dst_lds)[l] = reinterpret_cast<const u4 *>(buf)[l];
+}
+
+static std::atomic<int> g_unaligned[64];  // per device: 0 not probed, 1 any byte address works, 2 not (or forced)
+
+static bool run_unaligned_probe() {
+    constexpr int kB = 4096;
+    uint8_t *src = nullptr, *dst = nullptr, *dl = nullptr;
+    hipStream_t st = nullptr;
+    bool ok = hipMalloc(&src, kB) == hipSuccess && hipMalloc(&dst, kB) == hipSuccess && hipMalloc(&dl, kB) == hipSuccess &&
+              hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+    std::vector<uint8_t> h(kB), g(kB), gl(kB);
+    for (int i = 0; i < kB; ++i) h[i] = uint8_t(i * 73 + (i >> 8) + 1);
+    if (ok) {
+        ok = hipMemcpyAsync(src, h.data(), kB, hipMemcpyHostToDevice, st) == hipSuccess &&
+             hipMemsetAsync(dst, 0, kB, st) == hipSuccess;
+        if (ok) {
+            hipLaunchKernelGGL(unaligned_probe_kernel, dim3(1), dim3(64), 0, st, src, dst, dl);
+            ok = hipGetLastError() == hipSuccess &&
+                 hipMemcpyAsync(g.data(), dst, kB, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                 hipMemcpyAsync(gl.data(), dl, kB, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                 hipStreamSynchronize(st) == hipSuccess;
+        }
+    }
+    for (int l = 0; ok && l < 64; ++l) {
+        const int off = 1 + l % 15;
+        for (int b = 0; b < 16; ++b)
+            ok = ok && g[32 * l + 16 - off + b] == h[32 * l + off + b] && gl[16 * l + b] == h[32 * l + off + b];
+    }
+    if (st) (void)hipStreamDestroy(st);
+    for (uint8_t *x : {src, dst, dl})
+        if (x) (void)hipFree(x);
+    (void)hipGetLastError();  // a failed probe leaves no sticky error behind
+    return ok;
+}
+
+int probe_unaligned_vector_access(int device) {
+    if (device < 0 || device >= 64) return 0;
+    int v = g_unaligned[device].load();
+    if (v != 0) return v == 1;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
+    if ((v = g_unaligned[device].load()) != 0) return v == 1;
+    const char *e = getenv("RLNC_ASSUME_ALIGNED_ONLY");
+    const bool ok = !(e != nullptr && atoi(e) != 0) && run_unaligned_probe();
+    g_unaligned[device].store(ok ? 1 : 2);
+    return ok;
+}
+
+int unaligned_vector_access(int device) {
+    if (device < 0 || device >= 64) return -1;
+    const int v = g_unaligned[device].load();
+    return v == 0 ? -1 : v == 1;
+}
+
+bool unaligned_vector_ok() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    return g_unaligned[dev].load(std::memory_order_relaxed) == 1;
+}
 
 // ---------------------------------------------------------------------------------------------------
 // Realigned products.  A piece row is rarely 16-byte aligned: Encoder::new pads to L = ceil((len + 1) / k)
@@ -1874,7 +1962,8 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
 
 bool ragged_bsj_eligible(const uint8_t *in, const uint8_t *out, int64_t in_row, int64_t out_row, int64_t width,
                          int n_out) {
-    return al16(in) && al16(out) && al16(in_row) && al16(out_row) && width >= kBsjColBlock && n_out >= 4 &&
+    return (unaligned_vector_ok() || (al16(in) && al16(out) && al16(in_row) && al16(out_row))) && width >= kBsjColBlock &&
+           n_out >= 4 &&
            in_row < (int64_t(1) << 32) && out_row < (int64_t(1) << 32);
 }
 
@@ -1928,7 +2017,7 @@ hipError_t launch_final_data_len(const uint8_t *data, int64_t obj_stride, int64_
                                  int32_t invalid_code, hipStream_t s) {
     if (n_obj <= 0) return hipSuccess;
     hipError_t e;
-    if (al16(data) && (n_obj == 1 || al16(obj_stride)))
+    if (unaligned_vector_ok() || (al16(data) && (n_obj == 1 || al16(obj_stride))))
         hipLaunchKernelGGL(last_nonzero_kernel<true>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, scratch,
                            nullptr, 0);
     else

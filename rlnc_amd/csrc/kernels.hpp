@@ -48,6 +48,12 @@ enum class MatmulVariant : int {
 // shapes that variant hands to the perm kernel).  launch_matmul fails with hipErrorInvalidValue when a
 // BitSliced launch gets less.
 size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v);
+// Byte-misaligned 16-byte vector memory access (kernels.hip): probe_unaligned_vector_access runs the check on the
+// current device once (synchronous; rlnc_context_create) and returns whether it holds; unaligned_vector_access(dev)
+// is 1 / 0, or -1 before the probe; unaligned_vector_ok() is the current device's result.
+int probe_unaligned_vector_access(int device);
+int unaligned_vector_access(int device);
+bool unaligned_vector_ok();
 hipError_t launch_matmul(const MatmulParams &p, hipStream_t stream, MatmulVariant v = MatmulVariant::Perm,
                          void *scratch = nullptr, size_t scratch_bytes = 0);
 

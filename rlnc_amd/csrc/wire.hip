@@ -218,7 +218,8 @@ int ragged_matmul(rlnc_context *ctx, const std::vector<MatmulJob> &jobs) {
             d.n_in = j.n_in;
             d.row_tiles = (j.n_out + rlnc::kRaggedPermRows - 1) / rlnc::kRaggedPermRows;
             d.col_blocks = int((d.width + rlnc::kRaggedColBlock - 1) / rlnc::kRaggedColBlock);
-            d.aligned = al16p(j.in + full) && al16p(j.out + full) && (j.in_row & 15) == 0 && (j.out_row & 15) == 0;
+            d.aligned = rlnc::unaligned_vector_ok() ||
+                        (al16p(j.in + full) && al16p(j.out + full) && (j.in_row & 15) == 0 && (j.out_row & 15) == 0);
             perm.push_back(d);
         }
     }

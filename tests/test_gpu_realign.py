@@ -1,9 +1,15 @@
-"""Realigned products (kernels.hip `realign_plan` / `realign_rows_kernel`): operands whose rows are not 16-byte
-aligned -- the common case, since Encoder::new pads to L = ceil((len + 1) / k) (encoder.rs:93-95) and a coded
-piece's data starts at byte k of its (k + L)-byte row -- are copied into aligned scratch rows around the bit-sliced
-and stream kernels.  Checked bit for bit against the numpy checker and against the same product on aligned copies,
-with the bytes around every misaligned output row (a coded piece's coefficient header) left untouched."""
+"""Products on rows that are not 16-byte aligned -- the common case, since Encoder::new pads to
+L = ceil((len + 1) / k) (encoder.rs:93-95) and a coded piece's data starts at byte k of its (k + L)-byte row.  On a
+device whose queues execute 16-byte vector memory instructions at any byte address (probed when the first context is
+created: rlnc_device_unaligned_vector_access) they take the vector kernels directly; elsewhere (or with
+RLNC_ASSUME_ALIGNED_ONLY=1) kernels.hip's realigned path copies them through 16-byte scratch rows
+(`realign_plan` / `realign_rows_kernel`).  Both paths checked bit for bit against the numpy checker and against the
+same product on aligned copies, with the bytes around every misaligned output row (a coded piece's coefficient
+header) left untouched; the realigned path in a child process with the variable set."""
 import ctypes as C
+import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -127,3 +133,34 @@ def test_realigned_chunks_match_aligned(ctx):
     cols = slice(W - 4099, W)
     want = np_matmul(host(coef[1]), host(src_al[1, :, cols]))
     assert np.array_equal(host(got[1, :, cols]), want)
+
+
+def test_unaligned_probe_reports(ctx):
+    v = ctx.lib.rlnc_device_unaligned_vector_access(0)
+    assert v in (0, 1), v
+    assert ctx.lib.rlnc_device_unaligned_vector_access(63) == -1  # no context there: not probed
+
+
+def _forced_main():
+    """Child process (RLNC_ASSUME_ALIGNED_ONLY=1): every CASES product and the header framing on the realigned path."""
+    import rlnc_amd
+
+    c = rlnc_amd.Context(0)
+    assert c.lib.rlnc_device_unaligned_vector_access(0) == 0
+    for case in CASES:
+        test_realigned_matmul(c, *case)
+    test_realigned_headers(c)
+    test_realigned_chunks_match_aligned(c)
+    print("forced realigned path ok")
+
+
+def test_realigned_path_forced():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RLNC_ASSUME_ALIGNED_ONLY="1", PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--forced"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "forced realigned path ok" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+
+
+if __name__ == "__main__" and "--forced" in sys.argv:
+    _forced_main()
