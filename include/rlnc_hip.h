@@ -281,7 +281,8 @@ int rlnc_encoder_new_device(rlnc_context *ctx, const uint8_t *data_dev, size_t d
 /* Ragged batches: every object with its own shape and buffers (device pointers; strides 0 = dense), as a sender or
  * receiver holding pieces of many objects has them.  Each kernel stage is one launch over a device-side descriptor
  * table, whatever the number of objects and shapes (the matmul stage: <= 4 launches -- block addresses, the
- * bit-sliced program for <= 32 and > 32 output rows, the perm kernel for < 4 KiB tails and unaligned operands).
+ * bit-sliced program for <= 32 and > 32 output rows, the perm kernel for < 4 KiB tails -- and for misaligned
+ * operands on a device without unaligned vector access, rlnc_device_unaligned_vector_access).
  * Asynchronous on the context stream.  Error checks run over all descriptors before anything is launched.
  * rlnc_encode_ragged: n coded pieces coeffs ‖ data per object (encoder.rs:241-250 × n). */
 typedef struct rlnc_object_desc {
