@@ -694,6 +694,9 @@ def run_gpu(args, dist: Dist):
         "n_gpus": dist.world,
         "world_size_initialised": dist.initialised_world(),
         "process_group_backend": dist.pg.get_backend() if dist.pg else None,
+        # 1: the device runs 16-byte vector memory instructions at any byte address (probed at context creation;
+        # misaligned rows take the vector kernels directly), 0: they go through realigning copies
+        "unaligned_vector_access": int(ctx.lib.rlnc_device_unaligned_vector_access(dist.local_rank)),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
