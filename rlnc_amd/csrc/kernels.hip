@@ -1704,7 +1704,12 @@ int probe_unaligned_vector_access(int device) {
     std::lock_guard<std::mutex> lock(mu);
     if ((v = g_unaligned[device].load()) != 0) return v == 1;
     const char *e = getenv("RLNC_ASSUME_ALIGNED_ONLY");
+    // relaxed capture mode on this thread while probing, so a context created while another stream of the process
+    // is being captured neither fails nor invalidates that capture (the probe's allocations are not stream work)
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    const bool swapped = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
     const bool ok = !(e != nullptr && atoi(e) != 0) && run_unaligned_probe();
+    if (swapped) (void)hipThreadExchangeStreamCaptureMode(&mode);
     g_unaligned[device].store(ok ? 1 : 2);
     return ok;
 }
