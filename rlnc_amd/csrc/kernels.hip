@@ -508,6 +508,10 @@ hipError_t launch_stream(const MatmulParams &p, int64_t full, hipStream_t s) {
     const int row_tiles = (p.n_out + NT - 1) / NT;
     const int col_blocks = int(full / kColBlock);
     if (p.n_in <= kKC) {
+        // a launch too small to fill the device (one coded piece of a small object: latency-bound) keeps four rows
+        // in flight per lane over one 4 KiB slot instead of one row pair over two
+        if (stream_form() == 11 && int64_t(p.n_obj) * row_tiles * col_blocks < 1024)
+            return launch_stream3<NT, 4, 1, true>(q, row_tiles, col_blocks, s);
         switch (stream_form()) {
             case 11: return launch_stream3<NT, 1, 2, true>(q, row_tiles, col_blocks, s);
 #ifdef RLNC_AB_VARIANTS  // the other measured forms (profiles/r02_stream_ab.txt), diagnostic builds only
@@ -1952,10 +1956,13 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
 #endif
     // narrow (< one 4 KiB column block, e.g. the ragged tail of a recode over k + L bytes): the work is the
     // sources x rows chain of one block, so split the rows over many workgroups (2 rows each)
-    if (p.width < kColBlock && p.n_out > 2) {
+    // (1-2 rows too while the sources are few, e.g. the short tail of one recoded piece: 107 -> 80 us per
+    // Recoder::recode_with_buf call at 16 MiB / k = 64 over 32 pieces with the small-launch stream form below; over 128+
+    // sources the perm kernel's chunked tables were faster: profiles/r03_object_api_rates.jsonl)
+    if (p.width < kColBlock && (p.n_out > 2 || p.n_in <= kKC)) {
         if (v == MatmulVariant::Perm && narrow_lds_bytes(p.n_in) <= kNarrowMaxLds && narrow_form() == 1)
             return launch_narrow(p, aligned, s);
-        return launch_nt<2>(p, s, v, aligned);
+        if (p.n_out > 2) return launch_nt<2>(p, s, v, aligned);
     }
     if (p.n_out <= 1) return launch_nt<1>(p, s, v, aligned);
     if (p.n_out <= 2) return launch_nt<2>(p, s, v, aligned);
