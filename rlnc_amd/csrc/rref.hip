@@ -1431,8 +1431,12 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
 #pragma unroll
         for (int t = 0; t < B; ++t) {
             if (t < c) {
-                // forward: quotients are the block-reduced row's bytes r+s (s < t), read before any update
+                // forward: quotients are the block-reduced row's bytes r+s (s < t), read before any update.  The
+                // backward step's quotients y_s[r+t] (s < t) do not change during this piece's forward pass either,
+                // so their table reads are issued here too: one dependent LDS round trip less per piece
                 uint32_t acc = y[t];
+                uint4 b4[B];
+                uint32_t b2[B];
                 {
                     uint4 f4[B];
                     uint32_t f2[B];
@@ -1441,6 +1445,12 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
                         const uint32_t q = byte_of(y[t], (r + s2) >> 2, (r + s2) & 3);
                         f4[s2] = *reinterpret_cast<const uint4 *>(tab + q * kTabDw);
                         f2[s2] = tab[q * kTabDw + 4];
+                    }
+#pragma unroll
+                    for (int s2 = 0; s2 < t; ++s2) {
+                        const uint32_t qb = byte_of(y[s2], (r + t) >> 2, (r + t) & 3);
+                        b4[s2] = *reinterpret_cast<const uint4 *>(tab + qb * kTabDw);
+                        b2[s2] = tab[qb * kTabDw + 4];
                     }
 #pragma unroll
                     for (int s2 = 0; s2 < t; ++s2) acc ^= mul4t(f4[s2], f2[s2], y[s2]);
@@ -1455,14 +1465,6 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_block_kernel(RrefParams p) {
                     if (w == ((r + t) >> 2)) y[t] = (y[t] & ~(0xFFu << (8 * ((r + t) & 3)))) | (1u << (8 * ((r + t) & 3)));
                     // backward inside the block: y_s ^= y_s[r+t]·y_t (s < t), y_t's selectors shared
                     const uint32_t e0 = y[t] & 0x07070707u, e1 = (y[t] >> 3) & 0x07070707u, e2 = (y[t] >> 6) & 0x03030303u;
-                    uint4 b4[B];
-                    uint32_t b2[B];
-#pragma unroll
-                    for (int s2 = 0; s2 < t; ++s2) {
-                        const uint32_t qb = byte_of(y[s2], (r + t) >> 2, (r + t) & 3);
-                        b4[s2] = *reinterpret_cast<const uint4 *>(tab + qb * kTabDw);
-                        b2[s2] = tab[qb * kTabDw + 4];
-                    }
 #pragma unroll
                     for (int s2 = 0; s2 < t; ++s2)
                         y[s2] = xor3(y[s2], __builtin_amdgcn_perm(b4[s2].y, b4[s2].x, e0),
