@@ -401,12 +401,71 @@ __device__ __forceinline__ Sel selectors64(uint4 x) {
 
 // One-block streaming form with VW 16-byte slots per lane (slot v at column v * 4 KiB of a VW * 4 KiB block:
 // every table read feeds VW x the bytes, VW x PF loads in flight per lane) and optionally 64-bit-shift selectors.
+// tail > 0: the grid carries one more workgroup per (object, row tile) after the blocks, for the ragged tail of
+// `tail` (< 4 KiB) bytes at column p.width -- saves the tail's own launch (≈ 13 us of a one-piece encode call)
+template <int NT>
+__device__ __forceinline__ void stream_tail(const MatmulParams &p, int row_tiles, int64_t tail, int64_t u,
+                                            const uint4 (*s_t01)[NT], const uint32_t (*s_t2)[NT]) {
+    const int obj = int(u / row_tiles), rt = int(u % row_tiles);
+    const int row0 = rt * NT, rows_here = min(NT, p.n_out - row0), kc = p.n_in;
+    const int64_t col = p.width + int64_t(threadIdx.x) * kBytesPerThread;
+    const int nbytes = int(max<int64_t>(0, min<int64_t>(kBytesPerThread, p.width + tail - col)));
+    if (nbytes == 0) return;
+    const uint8_t *rowp = p.in + int64_t(obj) * p.in_obj + col;
+    uint32_t acc[NT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0u;
+    for (int j0 = 0; j0 < kc; j0 += 4) {  // four source rows in flight
+        uint4 x[4];
+#pragma unroll
+        for (int u2 = 0; u2 < 4; ++u2) x[u2] = load16<true>(rowp + int64_t(min(j0 + u2, kc - 1)) * p.in_row, nbytes);
+#pragma unroll
+        for (int u2 = 0; u2 < 4; ++u2) {
+            const int j = j0 + u2;
+            if (j >= kc) break;
+            const Sel a = selectors(x[u2]);
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                const uint4 ta = s_t01[j][i];
+                const uint32_t ta2 = s_t2[j][i];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    acc[i][q] = xor3(xor3(acc[i][q], vperm(ta.y, ta.x, a.s0[q]), vperm(ta.w, ta.z, a.s1[q])),
+                                     vperm(ta2, ta2, a.s2[q]), 0u);
+            }
+        }
+    }
+    uint8_t *outp = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + col;
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+        if (i < rows_here)
+            store16<true>(outp + int64_t(i) * p.out_row, make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]), nbytes);
+}
+
 template <int NT, int PF, int VW, bool SH64>
-__global__ __launch_bounds__(kThreads) void gf_matmul_stream3_kernel(MatmulParams p, int row_tiles, int col_blocks) {
+__global__ __launch_bounds__(kThreads) void gf_matmul_stream3_kernel(MatmulParams p, int row_tiles, int col_blocks,
+                                                                     int64_t tail) {
     __shared__ uint4 s_t01[kKC][NT];
     __shared__ uint32_t s_t2[kKC][NT];
+    const int64_t blocks = int64_t(p.n_obj) * row_tiles * col_blocks;
+    if (int64_t(blockIdx.x) >= blocks) {  // a ragged-tail workgroup: its tables, then the tail
+        const int64_t u = int64_t(blockIdx.x) - blocks;
+        const int rt = int(u % row_tiles), obj = int(u / row_tiles), row0 = rt * NT;
+        const int rows_here = min(NT, p.n_out - row0);
+        const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
+        for (int e = threadIdx.x; e < kKC * NT; e += kThreads) {
+            const int i = e % NT, j = e / NT;
+            const uint8_t c = (i < rows_here && j < p.n_in) ? coef_base[int64_t(i) * p.coef_row + j] : uint8_t(0);
+            const PermTable pt = make_perm_table(c);
+            s_t01[j][i] = make_uint4(pt.t0lo, pt.t0hi, pt.t1lo, pt.t1hi);
+            s_t2[j][i] = pt.t2;
+        }
+        __syncthreads();
+        stream_tail<NT>(p, row_tiles, tail, u, s_t01, s_t2);
+        return;
+    }
     int rt, cb, obj;
-    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    decode_block(int(blocks), row_tiles, col_blocks, rt, cb, obj);
     const int row0 = rt * NT;
     const int rows_here = min(NT, p.n_out - row0);
     const int kc = p.n_in;
@@ -473,12 +532,12 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_stream3_kernel(MatmulParam
 }
 
 template <int NT, int PF, int VW, bool SH64>
-hipError_t launch_stream3(const MatmulParams &q, int row_tiles, int col_blocks, hipStream_t s) {
-    if (col_blocks % VW) return launch_stream3<NT, PF, 1, SH64>(q, row_tiles, col_blocks, s);
-    const int64_t total = int64_t(q.n_obj) * row_tiles * (col_blocks / VW);
+hipError_t launch_stream3(const MatmulParams &q, int row_tiles, int col_blocks, hipStream_t s, int64_t tail) {
+    if (col_blocks % VW) return launch_stream3<NT, PF, 1, SH64>(q, row_tiles, col_blocks, s, tail);
+    const int64_t total = int64_t(q.n_obj) * row_tiles * (col_blocks / VW) + (tail > 0 ? int64_t(q.n_obj) * row_tiles : 0);
     if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
     hipLaunchKernelGGL((gf_matmul_stream3_kernel<NT, PF, VW, SH64>), dim3(unsigned(total)), dim3(kThreads), 0, s, q,
-                       row_tiles, col_blocks / VW);
+                       row_tiles, col_blocks / VW, tail);
     return hipGetLastError();
 }
 
@@ -501,27 +560,31 @@ int stream_form() {
     return f;
 }
 
+// tail_done: the stream3 forms also take the ragged tail (p.width - full bytes) in the same launch
 template <int NT>
-hipError_t launch_stream(const MatmulParams &p, int64_t full, hipStream_t s) {
+hipError_t launch_stream(const MatmulParams &p, int64_t full, hipStream_t s, bool &tail_done) {
     MatmulParams q = p;
     q.width = full;
     const int row_tiles = (p.n_out + NT - 1) / NT;
     const int col_blocks = int(full / kColBlock);
+    const int64_t tail = p.width - full;
+    tail_done = false;
     if (p.n_in <= kKC) {
+        tail_done = true;
         // a launch too small to fill the device (one coded piece of a small object: latency-bound) keeps four rows
         // in flight per lane over one 4 KiB slot instead of one row pair over two
         if (stream_form() == 11 && int64_t(p.n_obj) * row_tiles * col_blocks < 1024)
-            return launch_stream3<NT, 4, 1, true>(q, row_tiles, col_blocks, s);
+            return launch_stream3<NT, 4, 1, true>(q, row_tiles, col_blocks, s, tail);
         switch (stream_form()) {
-            case 11: return launch_stream3<NT, 1, 2, true>(q, row_tiles, col_blocks, s);
+            case 11: return launch_stream3<NT, 1, 2, true>(q, row_tiles, col_blocks, s, tail);
 #ifdef RLNC_AB_VARIANTS  // the other measured forms (profiles/r02_stream_ab.txt), diagnostic builds only
-            case 8: return launch_stream3<NT, 2, 1, true>(q, row_tiles, col_blocks, s);
-            case 9: return launch_stream3<NT, 2, 2, true>(q, row_tiles, col_blocks, s);
-            case 10: return launch_stream3<NT, 2, 2, false>(q, row_tiles, col_blocks, s);
-            case 12: return launch_stream3<NT, 3, 1, true>(q, row_tiles, col_blocks, s);
-            case 13: return launch_stream3<NT, 2, 1, false>(q, row_tiles, col_blocks, s);
+            case 8: return launch_stream3<NT, 2, 1, true>(q, row_tiles, col_blocks, s, tail);
+            case 9: return launch_stream3<NT, 2, 2, true>(q, row_tiles, col_blocks, s, tail);
+            case 10: return launch_stream3<NT, 2, 2, false>(q, row_tiles, col_blocks, s, tail);
+            case 12: return launch_stream3<NT, 3, 1, true>(q, row_tiles, col_blocks, s, tail);
+            case 13: return launch_stream3<NT, 2, 1, false>(q, row_tiles, col_blocks, s, tail);
 #endif
-            default: break;
+            default: tail_done = false; break;
         }
     }
     const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
@@ -1904,9 +1967,11 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
     if (jump && aligned && p.n_out <= 3 && p.width >= kColBlock) {
         // one to three coded pieces per source pass: HBM-bound, streamed with deep prefetch
         const int64_t full = (p.width / kColBlock) * kColBlock;
-        hipError_t e = p.n_out == 1 ? launch_stream<1>(p, full, s)
-                                    : p.n_out == 2 ? launch_stream<2>(p, full, s) : launch_stream<3>(p, full, s);
-        if (e != hipSuccess || full == p.width) return e;
+        bool tail_done = false;
+        hipError_t e = p.n_out == 1   ? launch_stream<1>(p, full, s, tail_done)
+                       : p.n_out == 2 ? launch_stream<2>(p, full, s, tail_done)
+                                      : launch_stream<3>(p, full, s, tail_done);
+        if (e != hipSuccess || full == p.width || tail_done) return e;
         MatmulParams t = p;
         t.in = p.in + full;
         t.out = p.out + full;
