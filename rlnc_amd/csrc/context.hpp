@@ -108,6 +108,20 @@ struct CallWs {
     }
 };
 
+// Staging ring of the object API's host -> device piece uploads (Decoder::decode): a call copies its piece into a
+// pinned slot and returns; the DMA runs behind it on the context's one upload stream, so a slot's event, whenever it
+// was last recorded, is ordered after every upload issued before it.  Pieces larger than a chunk take several slots.
+struct UpSlot {
+    std::mutex mu;
+    PinBuf buf;
+    hipEvent_t ev = nullptr;  // the slot's last DMA (the slot may be rewritten once it has run)
+    ~UpSlot() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+};
+constexpr int kUpSlots = 8;
+constexpr size_t kUpChunk = size_t(4) << 20;
+
 }  // namespace rlnc::eng
 
 using rlnc::eng::set_error;
@@ -152,6 +166,10 @@ struct rlnc_context {
     // exactly its captured bytes); reserved by eager calls, since nothing may be allocated inside a capture
     std::vector<std::unique_ptr<DevBuf>> cap_arenas;
     size_t cap_used = 0;
+    rlnc::eng::UpSlot up[rlnc::eng::kUpSlots];
+    std::atomic<unsigned> up_next{0};
+    std::mutex up_mu;
+    hipStream_t up_stream = nullptr;
 
     void retain() { refs.fetch_add(1, std::memory_order_relaxed); }
     void release() {
@@ -164,6 +182,10 @@ struct rlnc_context {
                 (void)hipStreamDestroy(x);
             }
         hs_slots.clear();
+        if (up_stream) {
+            (void)hipStreamSynchronize(up_stream);
+            (void)hipStreamDestroy(up_stream);
+        }
         if (tab_ev) (void)hipEventDestroy(tab_ev);
         if (own) (void)hipStreamDestroy(own);
         delete this;  // the buffers' destructors free on this device
@@ -194,6 +216,48 @@ struct rlnc_context {
             return set_error(RLNC_ERR_INVALID_ARGUMENT,
                              "this context's workspaces are bound to a captured HIP graph and cannot grow");
         return b.ensure(bytes);
+    }
+    int upload_stream(hipStream_t &s) {
+        std::lock_guard<std::mutex> lock(up_mu);
+        if (!up_stream) HIP_TRY(hipStreamCreateWithFlags(&up_stream, hipStreamNonBlocking));
+        s = up_stream;
+        return RLNC_OK;
+    }
+    // host -> device copy of n bytes through the staging ring on the upload stream: returns once the bytes are in
+    // pinned memory (src may then be reused), the DMAs still queued; *slot = the ring slot of the last chunk
+    int upload(uint8_t *dst, const uint8_t *src, size_t n, int *slot) {
+        using rlnc::eng::kUpChunk;
+        hipStream_t s = nullptr;
+        if (int st = upload_stream(s)) return st;
+        for (size_t o = 0; o < n; o += kUpChunk) {
+            const size_t c = std::min(kUpChunk, n - o);
+            const int i = int(up_next.fetch_add(1, std::memory_order_relaxed) % rlnc::eng::kUpSlots);
+            rlnc::eng::UpSlot &u = up[i];
+            std::lock_guard<std::mutex> lock(u.mu);
+            if (!u.ev)
+                HIP_TRY(hipEventCreateWithFlags(&u.ev, hipEventDisableTiming));
+            else
+                HIP_TRY(hipEventSynchronize(u.ev));  // the slot's previous DMA has read it
+            if (int st = u.buf.ensure(c)) return st;
+            std::memcpy(u.buf.p, src + o, c);
+            HIP_TRY(hipMemcpyAsync(dst + o, u.buf.p, c, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipEventRecord(u.ev, s));
+            *slot = i;
+        }
+        return RLNC_OK;
+    }
+    // order stream s after every upload up to the one that used `slot` (see UpSlot)
+    int upload_wait(int slot, hipStream_t s) {
+        rlnc::eng::UpSlot &u = up[slot];
+        std::lock_guard<std::mutex> lock(u.mu);
+        HIP_TRY(hipStreamWaitEvent(s, u.ev, 0));
+        return RLNC_OK;
+    }
+    int upload_sync(int slot) {
+        rlnc::eng::UpSlot &u = up[slot];
+        std::lock_guard<std::mutex> lock(u.mu);
+        HIP_TRY(hipEventSynchronize(u.ev));
+        return RLNC_OK;
     }
     // a call workspace, ordered after the work already enqueued on the context stream
     int lease(std::unique_ptr<CallWs> &ws) {

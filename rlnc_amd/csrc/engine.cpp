@@ -71,11 +71,16 @@ struct rlnc_decoder {
     std::unique_ptr<Elimination> elim;
     uint8_t *store = nullptr;  // slot rows × stride (received data rows still referenced by E)
     size_t store_slots = 0;
+    // the context's upload-ring slot of the last upload into store (Decoder::decode returns once its piece is staged,
+    // before the DMA): every later use of store, on whichever stream, is ordered after it
+    int up_slot = -1;
     void bind(rlnc_context *c) {
         ctx = c;
         c->retain();
     }
+    int order(hipStream_t s) const { return up_slot >= 0 ? ctx->upload_wait(up_slot, s) : RLNC_OK; }
     ~rlnc_decoder() {
+        if (up_slot >= 0) (void)ctx->upload_sync(up_slot);
         if (store) (void)hipFree(store);
         if (ctx) ctx->release();
     }
@@ -635,7 +640,7 @@ int rlnc_decoder_clone(const rlnc_decoder *d, rlnc_decoder **out) {
         HIP_TRY(hipMalloc(&c->store, d->store_slots * d->stride));
         c->store_slots = d->store_slots;
         Lease ws(d->ctx);
-        if ((st = ws.acquire())) return st;
+        if ((st = ws.acquire()) || (st = d->order(ws->stream))) return st;
         HIP_TRY(hipMemcpyAsync(c->store, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ws->stream));
         HIP_TRY(hipStreamSynchronize(ws->stream));
     }
@@ -645,25 +650,32 @@ int rlnc_decoder_clone(const rlnc_decoder *d, rlnc_decoder **out) {
 
 void rlnc_decoder_free(rlnc_decoder *d) { delete d; }
 
-static int decoder_store_slot(rlnc_decoder *d, CallWs *ws, int slot, const uint8_t *src, hipMemcpyKind kind) {
+// s: the stream of the row copy (host pieces: the context's upload stream, where a store reallocation then also runs)
+static int decoder_store_slot(rlnc_decoder *d, hipStream_t s, int slot, const uint8_t *src, hipMemcpyKind kind) {
+    if (int st = d->order(s)) return st;
     if (size_t(slot) >= d->store_slots) {
         size_t ns = std::max(d->elim->slots(), size_t(slot) + 1);
         uint8_t *n = nullptr;
         HIP_TRY(hipMalloc(&n, ns * d->stride));
         if (d->store) {
-            HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ws->stream));
-            HIP_TRY(hipStreamSynchronize(ws->stream));
+            HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, s));
+            HIP_TRY(hipStreamSynchronize(s));
             (void)hipFree(d->store);
         }
         d->store = n;
         d->store_slots = ns;
     }
-    HIP_TRY(hipMemcpyAsync(d->store + size_t(slot) * d->stride, src, d->L, kind, ws->stream));
-    HIP_TRY(hipStreamSynchronize(ws->stream));  // the caller may reuse the piece; the call is synchronous
+    uint8_t *row = d->store + size_t(slot) * d->stride;
+    if (kind == hipMemcpyHostToDevice)
+        // staged through pinned memory: the caller may reuse the piece when the call returns, no synchronisation
+        // (a pageable copy's cost 30 us per call for small pieces)
+        return d->ctx->upload(row, src, d->L, &d->up_slot);
+    HIP_TRY(hipMemcpyAsync(row, src, d->L, kind, s));
+    HIP_TRY(hipStreamSynchronize(s));  // the caller may reuse the piece; the call is synchronous
     return RLNC_OK;
 }
 
-static int decoder_decode_impl(rlnc_decoder *d, CallWs *ws, const uint8_t *coeffs_host, const uint8_t *data,
+static int decoder_decode_impl(rlnc_decoder *d, hipStream_t s, const uint8_t *coeffs_host, const uint8_t *data,
                                hipMemcpyKind kind) {
     int slot = -1;
     bool keep = false;
@@ -672,7 +684,7 @@ static int decoder_decode_impl(rlnc_decoder *d, CallWs *ws, const uint8_t *coeff
     d->received += 1;                                     // decoder.rs:107
     if (st == RLNC_OK) d->useful = d->elim->rank();       // :115
     if (keep)
-        if (int s2 = decoder_store_slot(d, ws, slot, data, kind)) return s2;
+        if (int s2 = decoder_store_slot(d, s, slot, data, kind)) return s2;
     return st;
 }
 
@@ -683,9 +695,9 @@ int rlnc_decoder_decode(rlnc_decoder *d, const uint8_t *piece, size_t len) {
     CHECK_ARG(piece != nullptr);
     int st = d->ctx->activate();
     if (st) return st;
-    Lease ws(d->ctx);
-    if ((st = ws.acquire())) return st;
-    return decoder_decode_impl(d, ws.ws.get(), piece, piece + d->k, hipMemcpyHostToDevice);
+    hipStream_t s = nullptr;  // no call workspace: the piece goes through the context's upload ring
+    if ((st = d->ctx->upload_stream(s))) return st;
+    return decoder_decode_impl(d, s, piece, piece + d->k, hipMemcpyHostToDevice);
 }
 
 int rlnc_decoder_decode_device(rlnc_decoder *d, const uint8_t *piece_dev, size_t len) {
@@ -700,7 +712,7 @@ int rlnc_decoder_decode_device(rlnc_decoder *d, const uint8_t *piece_dev, size_t
     HIP_TRY(hipMemcpyAsync(ws->pin_c.p, piece_dev, d->k, hipMemcpyDeviceToHost, ws->stream));
     HIP_TRY(hipStreamSynchronize(ws->stream));
     std::vector<uint8_t> coeffs(ws->pin_c.as<uint8_t>(), ws->pin_c.as<uint8_t>() + d->k);
-    return decoder_decode_impl(d, ws.ws.get(), coeffs.data(), piece_dev + d->k, hipMemcpyDeviceToDevice);
+    return decoder_decode_impl(d, ws->stream, coeffs.data(), piece_dev + d->k, hipMemcpyDeviceToDevice);
 }
 
 int rlnc_decoder_is_already_decoded(const rlnc_decoder *d) { return d && d->elim->decoded() ? 1 : 0; }
@@ -715,6 +727,7 @@ size_t rlnc_decoder_get_remaining_piece_count(const rlnc_decoder *d) { return d 
 static int decoder_apply(rlnc_decoder *d, CallWs *ws, uint8_t *out_dev) {
     const size_t slots = d->elim->slots();
     int st;
+    if ((st = d->order(ws->stream))) return st;
     if ((st = ws->pin_b.ensure(d->k * slots)) || (st = ws->coef.ensure(d->k * slots))) return st;
     d->elim->transform(ws->pin_b.as<uint8_t>(), slots);
     HIP_TRY(hipMemcpyAsync(ws->coef.p, ws->pin_b.p, d->k * slots, hipMemcpyHostToDevice, ws->stream));

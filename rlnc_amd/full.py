@@ -256,10 +256,10 @@ class Decoder:
     def get_decoded_data(self) -> np.ndarray:
         """Decoder::get_decoded_data — decoder.rs:136-159 (the Python object stays usable)."""
         cap = self.get_num_pieces_coded_together() * self.get_piece_byte_len()
-        out = np.zeros(cap, np.uint8)
+        out = np.empty(cap, np.uint8)
         n = C.c_size_t(0)
         check(self._lib.rlnc_decoder_get_decoded_data(self._h, _ptr(out), cap, C.byref(n)), self._lib)
-        return out[: n.value].copy()
+        return out[: n.value]  # a view: the caller owns it (Vec<u8>), no second pass over the object
 
     def get_decoded_data_device(self, out_dev_ptr: int, cap: int) -> int:
         n = C.c_size_t(0)

@@ -6,6 +6,8 @@
 * Objects outlive the context handle they were created with (the context is reference counted).
 * Batch calls without an explicit context on two torch streams: each stream gets its own context (its
   workspaces are stream-ordered), results against the numpy matmul.
+* Decoder::decode staged through the pinned upload ring (caller buffer reuse, chunked pieces, clone / drop with
+  uploads in flight).
 * The 8-wave (variant 8) program with padded row strides, a header slot and several objects.
 """
 import ctypes as C
@@ -143,6 +145,45 @@ def test_clone_encoder_decoder_recoder(ctx, orc):
     got = rec2.recode(x)
     assert np.array_equal(got, orc.recode(np.concatenate(seen), k + enc2.get_piece_byte_len(), k, x.draws[0]))
     assert np.array_equal(rec2.clone().recode(y), got)
+
+
+@pytest.mark.parametrize("data_len,k", [(1 << 20, 16), ((9 << 20) + 5, 2)])
+def test_decoder_staged_uploads(ctx, data_len, k):
+    """Decoder::decode returns once its piece is staged in pinned memory, before the DMA: one caller buffer reused
+    for every piece, interleaved decoders cycling the staging ring, pieces over the 4 MiB chunk (several slots per
+    piece), a clone and a drop taken with uploads still in flight -- every decoded object equals its source."""
+    from rlnc_amd.errors import RLNCError
+    from rlnc_amd.full import Decoder, Encoder
+
+    rng = np.random.default_rng(data_len)
+    datas = [rng.integers(0, 256, data_len + i, dtype=np.uint8) for i in range(3)]
+    encs = [Encoder.new(d, k, ctx=ctx) for d in datas]
+    decs = [Decoder.new(e.get_piece_byte_len(), k, ctx=ctx) for e in encs]
+    bufs = [np.empty(e.get_full_coded_piece_byte_len(), np.uint8) for e in encs]
+    clone = None
+    while not all(d.is_already_decoded() for d in decs):
+        for i, (e, d) in enumerate(zip(encs, decs)):
+            if d.is_already_decoded():
+                continue
+            bufs[i][:] = e.code(rng)  # the caller's one buffer, rewritten after every call
+            try:
+                d.decode(bufs[i])
+            except RLNCError as err:
+                assert err == RLNCError.PieceNotUseful
+            bufs[i][:] = 0
+            if i == 0 and clone is None and d.get_useful_piece_count() == k // 2:
+                clone = d.clone()
+                scratch = Decoder.new(e.get_piece_byte_len(), k, ctx=ctx)
+                scratch.decode(e.code(rng))
+                del scratch  # dropped with its upload possibly still queued
+    for d, data in zip(decs, datas):
+        assert np.array_equal(d.get_decoded_data(), data)
+    while not clone.is_already_decoded():
+        try:
+            clone.decode(encs[0].code(rng))
+        except RLNCError as err:
+            assert err == RLNCError.PieceNotUseful
+    assert np.array_equal(clone.get_decoded_data(), datas[0])
 
 
 def test_objects_outlive_their_context_handle(orc):
