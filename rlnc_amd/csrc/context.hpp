@@ -170,6 +170,13 @@ struct rlnc_context {
     std::atomic<unsigned> up_next{0};
     std::mutex up_mu;
     hipStream_t up_stream = nullptr;
+    // device blocks of dropped encoders / recoders / decoders, reused by the next object of a similar size: a
+    // hipMalloc + hipFree pair costs 0.1-0.6 ms per object, as much as a small object's whole decode
+    std::mutex blk_mu;
+    std::vector<std::pair<size_t, void *>> blk;  // (bytes, block), oldest first
+    size_t blk_bytes = 0;
+    static constexpr size_t kBlkCacheBytes = size_t(1) << 30;
+    static constexpr size_t kBlkCacheCount = 32;
 
     void retain() { refs.fetch_add(1, std::memory_order_relaxed); }
     void release() {
@@ -186,6 +193,7 @@ struct rlnc_context {
             (void)hipStreamSynchronize(up_stream);
             (void)hipStreamDestroy(up_stream);
         }
+        for (auto &b : blk) (void)hipFree(b.second);
         if (tab_ev) (void)hipEventDestroy(tab_ev);
         if (own) (void)hipStreamDestroy(own);
         delete this;  // the buffers' destructors free on this device
@@ -216,6 +224,48 @@ struct rlnc_context {
             return set_error(RLNC_ERR_INVALID_ARGUMENT,
                              "this context's workspaces are bound to a captured HIP graph and cannot grow");
         return b.ensure(bytes);
+    }
+    // an object's device block of at least n bytes (*cap = its size): a cached one when one fits (at most twice n
+    // plus 1 MiB), else hipMalloc
+    int obj_alloc(size_t n, uint8_t **p, size_t *cap) {
+        {
+            std::lock_guard<std::mutex> lock(blk_mu);
+            int best = -1;
+            for (int i = 0; i < int(blk.size()); ++i)
+                if (blk[i].first >= n && blk[i].first <= 2 * n + (size_t(1) << 20) &&
+                    (best < 0 || blk[i].first < blk[best].first))
+                    best = i;
+            if (best >= 0) {
+                *p = static_cast<uint8_t *>(blk[best].second);
+                *cap = blk[best].first;
+                blk_bytes -= *cap;
+                blk.erase(blk.begin() + best);
+                return RLNC_OK;
+            }
+        }
+        const size_t bytes = std::max<size_t>(n, 256);
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(p), bytes));
+        *cap = bytes;
+        return RLNC_OK;
+    }
+    // return an object's block (every upload into it already synchronised by the caller): the context stream's
+    // work (a _device call may still read it) is waited for, as hipFree would
+    void obj_free(void *p, size_t cap) {
+        if (!p) return;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (cap > kBlkCacheBytes / 4 || hipStreamIsCapturing(stream, &cs) != hipSuccess ||
+            cs != hipStreamCaptureStatusNone || hipStreamSynchronize(stream) != hipSuccess) {
+            (void)hipFree(p);
+            return;
+        }
+        std::lock_guard<std::mutex> lock(blk_mu);
+        blk.emplace_back(cap, p);
+        blk_bytes += cap;
+        while (blk_bytes > kBlkCacheBytes || blk.size() > kBlkCacheCount) {
+            (void)hipFree(blk.front().second);
+            blk_bytes -= blk.front().first;
+            blk.erase(blk.begin());
+        }
     }
     int upload_stream(hipStream_t &s) {
         std::lock_guard<std::mutex> lock(up_mu);

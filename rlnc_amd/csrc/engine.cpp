@@ -39,13 +39,14 @@ struct rlnc_encoder {
     rlnc_context *ctx = nullptr;
     size_t k = 0, L = 0, stride = 0;
     uint8_t *src = nullptr;  // k rows × stride
+    size_t src_cap = 0;      // bytes of the owned block
     bool owned = false;
     void bind(rlnc_context *c) {
         ctx = c;
         c->retain();
     }
     ~rlnc_encoder() {
-        if (owned && src) (void)hipFree(src);
+        if (owned && src) ctx->obj_free(src, src_cap);
         if (ctx) ctx->release();
     }
 };
@@ -54,12 +55,13 @@ struct rlnc_recoder {
     rlnc_context *ctx = nullptr;
     size_t k = 0, n = 0, full = 0, stride = 0;
     uint8_t *pieces = nullptr;  // n rows × stride (coeffs ‖ data)
+    size_t pieces_cap = 0;
     void bind(rlnc_context *c) {
         ctx = c;
         c->retain();
     }
     ~rlnc_recoder() {
-        if (pieces) (void)hipFree(pieces);
+        if (pieces) ctx->obj_free(pieces, pieces_cap);
         if (ctx) ctx->release();
     }
 };
@@ -70,7 +72,7 @@ struct rlnc_decoder {
     size_t received = 0, useful = 0;
     std::unique_ptr<Elimination> elim;
     uint8_t *store = nullptr;  // slot rows × stride (received data rows still referenced by E)
-    size_t store_slots = 0;
+    size_t store_slots = 0, store_cap = 0;
     // the context's upload-ring slot of the last upload into store (Decoder::decode returns once its piece is staged,
     // before the DMA): every later use of store, on whichever stream, is ordered after it
     int up_slot = -1;
@@ -81,7 +83,7 @@ struct rlnc_decoder {
     int order(hipStream_t s) const { return up_slot >= 0 ? ctx->upload_wait(up_slot, s) : RLNC_OK; }
     ~rlnc_decoder() {
         if (up_slot >= 0) (void)ctx->upload_sync(up_slot);
-        if (store) (void)hipFree(store);
+        if (store) ctx->obj_free(store, store_cap);
         if (ctx) ctx->release();
     }
 };
@@ -355,7 +357,7 @@ static int encoder_from_host(rlnc_context *ctx, const uint8_t *data, size_t len,
     e->L = L;
     e->stride = round16(L);
     e->owned = true;
-    HIP_TRY(hipMalloc(&e->src, k * e->stride));
+    if ((st = ctx->obj_alloc(k * e->stride, &e->src, &e->src_cap))) return st;
     Lease ws(ctx);
     if ((st = ws.acquire())) return st;
     // padded image: data, 0x81 marker, zeros (encoder.rs:98-99), laid out at a 16-B row stride
@@ -411,6 +413,7 @@ int rlnc::eng::encoder_adopt_device(rlnc_context *ctx, uint8_t *img, size_t k, s
     e->L = L;
     e->stride = stride;
     e->src = img;
+    e->src_cap = k * stride;
     e->owned = true;
     *out = e;
     return RLNC_OK;
@@ -432,7 +435,7 @@ int rlnc_encoder_clone(const rlnc_encoder *e, rlnc_encoder **out) {
     c->stride = e->stride;
     c->owned = e->owned;
     if (e->owned) {
-        HIP_TRY(hipMalloc(&c->src, e->k * e->stride));
+        if ((st = e->ctx->obj_alloc(e->k * e->stride, &c->src, &c->src_cap))) return st;
         Lease ws(e->ctx);
         if ((st = ws.acquire())) return st;
         HIP_TRY(hipMemcpyAsync(c->src, e->src, e->k * e->stride, hipMemcpyDeviceToDevice, ws->stream));
@@ -516,7 +519,7 @@ int rlnc_recoder_new(rlnc_context *ctx, const uint8_t *data, size_t len, size_t 
     r->n = n;
     r->full = full;
     r->stride = round16(full);
-    HIP_TRY(hipMalloc(&r->pieces, n * r->stride));
+    if ((st = ctx->obj_alloc(n * r->stride, &r->pieces, &r->pieces_cap))) return st;
     Lease ws(ctx);
     if ((st = ws.acquire())) return st;
     HIP_TRY(hipMemcpy2DAsync(r->pieces, r->stride, data, full, full, n, hipMemcpyHostToDevice, ws->stream));
@@ -538,7 +541,7 @@ int rlnc_recoder_clone(const rlnc_recoder *r, rlnc_recoder **out) {
     c->n = r->n;
     c->full = r->full;
     c->stride = r->stride;
-    HIP_TRY(hipMalloc(&c->pieces, r->n * r->stride));
+    if ((st = r->ctx->obj_alloc(r->n * r->stride, &c->pieces, &c->pieces_cap))) return st;
     Lease ws(r->ctx);
     if ((st = ws.acquire())) return st;
     HIP_TRY(hipMemcpyAsync(c->pieces, r->pieces, r->n * r->stride, hipMemcpyDeviceToDevice, ws->stream));
@@ -637,7 +640,7 @@ int rlnc_decoder_clone(const rlnc_decoder *d, rlnc_decoder **out) {
     c->elim.reset(new (std::nothrow) Elimination(*d->elim));
     if (!c->elim) return set_error(RLNC_ERR_OUT_OF_MEMORY, "decoder allocation");
     if (d->store_slots) {
-        HIP_TRY(hipMalloc(&c->store, d->store_slots * d->stride));
+        if ((st = d->ctx->obj_alloc(d->store_slots * d->stride, &c->store, &c->store_cap))) return st;
         c->store_slots = d->store_slots;
         Lease ws(d->ctx);
         if ((st = ws.acquire()) || (st = d->order(ws->stream))) return st;
@@ -654,15 +657,19 @@ void rlnc_decoder_free(rlnc_decoder *d) { delete d; }
 static int decoder_store_slot(rlnc_decoder *d, hipStream_t s, int slot, const uint8_t *src, hipMemcpyKind kind) {
     if (int st = d->order(s)) return st;
     if (size_t(slot) >= d->store_slots) {
-        size_t ns = std::max(d->elim->slots(), size_t(slot) + 1);
-        uint8_t *n = nullptr;
-        HIP_TRY(hipMalloc(&n, ns * d->stride));
-        if (d->store) {
-            HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, s));
-            HIP_TRY(hipStreamSynchronize(s));
-            (void)hipFree(d->store);
+        const size_t ns = std::max(d->elim->slots(), size_t(slot) + 1);
+        if (ns * d->stride > d->store_cap) {
+            uint8_t *n = nullptr;
+            size_t cap = 0;
+            if (int st = d->ctx->obj_alloc(ns * d->stride, &n, &cap)) return st;
+            if (d->store) {
+                HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, s));
+                HIP_TRY(hipStreamSynchronize(s));
+                d->ctx->obj_free(d->store, d->store_cap);
+            }
+            d->store = n;
+            d->store_cap = cap;
         }
-        d->store = n;
         d->store_slots = ns;
     }
     uint8_t *row = d->store + size_t(slot) * d->stride;
@@ -733,14 +740,19 @@ static int decoder_apply(rlnc_decoder *d, CallWs *ws, uint8_t *out_dev) {
     HIP_TRY(hipMemcpyAsync(ws->coef.p, ws->pin_b.p, d->k * slots, hipMemcpyHostToDevice, ws->stream));
     if (d->store_slots < slots) {
         // slots never stored were never referenced; give them zero rows so T × D is well defined
-        uint8_t *n = nullptr;
-        HIP_TRY(hipMalloc(&n, slots * d->stride));
-        HIP_TRY(hipMemsetAsync(n, 0, slots * d->stride, ws->stream));
-        if (d->store)
-            HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ws->stream));
-        HIP_TRY(hipStreamSynchronize(ws->stream));
-        if (d->store) (void)hipFree(d->store);
-        d->store = n;
+        if (slots * d->stride > d->store_cap) {
+            uint8_t *n = nullptr;
+            size_t cap = 0;
+            if ((st = d->ctx->obj_alloc(slots * d->stride, &n, &cap))) return st;
+            if (d->store)
+                HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ws->stream));
+            HIP_TRY(hipStreamSynchronize(ws->stream));
+            if (d->store) d->ctx->obj_free(d->store, d->store_cap);
+            d->store = n;
+            d->store_cap = cap;
+        }
+        HIP_TRY(hipMemsetAsync(d->store + d->store_slots * d->stride, 0, (slots - d->store_slots) * d->stride,
+                               ws->stream));
         d->store_slots = slots;
     }
     rlnc::MatmulParams p{};
