@@ -7,7 +7,47 @@
 #include "../../include/rlnc_hip.h"
 #include "gf256.hpp"
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+#include <immintrin.h>
+#endif
+
 namespace rlnc {
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+namespace {
+// d[0..n) ^= q·s[0..n) (or d = q·d when s == nullptr) 32 bytes at a time: the product of a byte is
+// lo[x & 15] ^ hi[x >> 4] (16-entry tables of q·v and q·(v << 4)), one vpshufb each.  The host runs this for every
+// pivot step of every Decoder::decode call (k = 128: ≈ 90 K products per call).
+__attribute__((target("avx2"))) void muladd_avx2(uint8_t *d, const uint8_t *s, size_t n, const uint8_t *mt) {
+    alignas(16) uint8_t lo[16], hi[16];
+    for (int v = 0; v < 16; ++v) {
+        lo[v] = mt[v];
+        hi[v] = mt[v << 4];
+    }
+    const __m256i tl = _mm256_broadcastsi128_si256(_mm_load_si128(reinterpret_cast<const __m128i *>(lo)));
+    const __m256i th = _mm256_broadcastsi128_si256(_mm_load_si128(reinterpret_cast<const __m128i *>(hi)));
+    const __m256i m = _mm256_set1_epi8(0x0f);
+    size_t c = 0;
+    for (; c + 32 <= n; c += 32) {
+        const __m256i x = _mm256_loadu_si256(reinterpret_cast<const __m256i *>((s ? s : d) + c));
+        const __m256i p = _mm256_xor_si256(_mm256_shuffle_epi8(tl, _mm256_and_si256(x, m)),
+                                           _mm256_shuffle_epi8(th, _mm256_and_si256(_mm256_srli_epi16(x, 4), m)));
+        __m256i *dp = reinterpret_cast<__m256i *>(d + c);
+        _mm256_storeu_si256(dp, s ? _mm256_xor_si256(_mm256_loadu_si256(dp), p) : p);
+    }
+    for (; c < n; ++c) d[c] = s ? uint8_t(d[c] ^ mt[s[c]]) : mt[d[c]];
+}
+const bool kHostAvx2 = __builtin_cpu_supports("avx2");
+}  // namespace
+#endif
+
+// d[0..n) ^= q·s[0..n), or d = q·d when s == nullptr (mt = the product table of q)
+static void gf_muladd(uint8_t *d, const uint8_t *s, size_t n, const uint8_t *mt) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    if (kHostAvx2 && n >= 32) return muladd_avx2(d, s, n, mt);
+#endif
+    for (size_t c = 0; c < n; ++c) d[c] = s ? uint8_t(d[c] ^ mt[s[c]]) : mt[d[c]];
+}
 
 const HostField &host_field() {
     static const HostField f;
@@ -38,8 +78,7 @@ void Elimination::row_muladd(size_t dst, size_t src, size_t from, uint8_t q) {
         for (size_t c = from; c < n; ++c) d[c] ^= s[c];
         return;
     }
-    const uint8_t *mt = host_field().mul[q];
-    for (size_t c = from; c < n; ++c) d[c] ^= mt[s[c]];
+    gf_muladd(d + from, s + from, n - from, host_field().mul[q]);
 }
 
 // clean_forward — decoder_matrix.rs:120-166
@@ -80,9 +119,7 @@ void Elimination::clean_backward() {
         }
         if (piv == 1) continue;  // :200-202
         m_[i * cols + i] = 1;    // :205
-        const uint8_t *mt = f.mul[inv_pivot];
-        uint8_t *r = &m_[i * cols];
-        for (size_t c = i + 1; c < cols; ++c) r[c] = mt[r[c]];  // :207-211
+        gf_muladd(&m_[i * cols + i + 1], nullptr, cols - i - 1, f.mul[inv_pivot]);  // :207-211
     }
 }
 
@@ -139,11 +176,15 @@ int Elimination::push(const uint8_t *coeffs, int *slot, bool *keep) {
     r[k_ + s] = 1;
     ++rows_;
     rref();  // decoder.rs:106
-    // a slot stays live while some row still references its piece
+    // a slot stays live while some row still references its piece (the rows' E parts OR-ed, row by row)
+    used_.assign(cap_, 0);
+    for (size_t q = 0; q < rows_; ++q) {
+        const uint8_t *e = &m_[q * stride() + k_];
+        for (size_t c = 0; c < cap_; ++c) used_[c] |= e[c];
+    }
     for (size_t c = 0; c < cap_; ++c) {
         if (!live_[c]) continue;
-        bool used = false;
-        for (size_t q = 0; q < rows_ && !used; ++q) used = m_[q * stride() + k_ + c] != 0;
+        const bool used = used_[c] != 0;
         if (!used && !fixed_) live_[c] = 0;
         if (c == s) *keep = used;
     }

@@ -53,6 +53,7 @@ class Elimination {
     bool fixed_;
     std::vector<uint8_t> m_;  // (k_ + 1) rows × stride()
     std::vector<uint8_t> live_;
+    std::vector<uint8_t> used_;  // push's scratch: OR of the rows' E parts
 };
 
 }  // namespace rlnc
