@@ -199,8 +199,9 @@ void rlnc_decoder_free(rlnc_decoder *dec);
 /* Decoder::decode (decoder.rs:96-118): Ok / PieceNotUseful / ReceivedAllPieces / InvalidPieceLength.
  * The accept/reject answer is immediate (exact replica of the diagonal-pivot RREF on the coefficient
  * block); the data rows are combined on the device when the data is requested.  The piece's data bytes are
- * staged in pinned memory before the call returns (the caller may reuse its buffer at once); their DMA runs on the
- * context's upload stream and every later use of the decoder is ordered after it. */
+ * staged in pinned memory before the call returns (the caller may reuse its buffer at once); staged pieces are
+ * copied to the device in batches on the context's upload stream, at the latest when the decoder's rows are next
+ * used (get_decoded_data, clone, drop), which is ordered after them. */
 int rlnc_decoder_decode(rlnc_decoder *dec, const uint8_t *full_coded_piece, size_t len);
 /* Same, piece already in HBM (only its k coefficient bytes are read back to the host). */
 int rlnc_decoder_decode_device(rlnc_decoder *dec, const uint8_t *piece_dev, size_t len);

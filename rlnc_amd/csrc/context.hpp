@@ -108,19 +108,34 @@ struct CallWs {
     }
 };
 
-// Staging ring of the object API's host -> device piece uploads (Decoder::decode): a call copies its piece into a
-// pinned slot and returns; the DMA runs behind it on the context's one upload stream, so a slot's event, whenever it
-// was last recorded, is ordered after every upload issued before it.  Pieces larger than a chunk take several slots.
+// Staging ring of the object API's host -> device piece uploads (Decoder::decode): a call copies its piece into the
+// open pinned slot and returns.  A slot collects pieces until it is full or one of its decoders needs its rows on the
+// device; then it is flushed -- one DMA per run of consecutive store rows, queued on the context's one upload stream
+// -- and its event recorded.  All DMAs run on that one stream, so a slot's event, whenever it was last recorded,
+// follows every upload flushed before it.  Pieces larger than a slot take several.
+struct UpRun {
+    uint8_t *dst;
+    size_t off, len;  // bytes [off, off + len) of the slot go to dst
+};
 struct UpSlot {
-    std::mutex mu;
     PinBuf buf;
-    hipEvent_t ev = nullptr;  // the slot's last DMA (the slot may be rewritten once it has run)
+    hipEvent_t ev = nullptr;  // the slot's last flush (the slot may be rewritten once it has run)
+    std::vector<UpRun> runs;  // staged, not yet flushed
+    size_t used = 0;
+    unsigned gen = 0;  // bumped each time the slot is reopened
+    bool open = false;
     ~UpSlot() {
         if (ev) (void)hipEventDestroy(ev);
     }
 };
 constexpr int kUpSlots = 8;
 constexpr size_t kUpChunk = size_t(4) << 20;
+constexpr size_t kUpRuns = 256;  // runs per slot before it is flushed
+// where a decoder's last piece was staged: ring slot and its generation then
+struct UpTicket {
+    int slot = -1;
+    unsigned gen = 0;
+};
 
 }  // namespace rlnc::eng
 
@@ -167,8 +182,8 @@ struct rlnc_context {
     std::vector<std::unique_ptr<DevBuf>> cap_arenas;
     size_t cap_used = 0;
     rlnc::eng::UpSlot up[rlnc::eng::kUpSlots];
-    std::atomic<unsigned> up_next{0};
-    std::mutex up_mu;
+    int up_cur = 0;       // the slot being filled
+    std::mutex up_mu;     // guards the ring and the upload stream
     hipStream_t up_stream = nullptr;
     // device blocks of dropped encoders / recoders / decoders, reused by the next object of a similar size: a
     // hipMalloc + hipFree pair costs 0.1-0.6 ms per object, as much as a small object's whole decode
@@ -267,46 +282,86 @@ struct rlnc_context {
             blk.erase(blk.begin());
         }
     }
+    int upload_stream_locked() {
+        if (!up_stream) HIP_TRY(hipStreamCreateWithFlags(&up_stream, hipStreamNonBlocking));
+        return RLNC_OK;
+    }
     int upload_stream(hipStream_t &s) {
         std::lock_guard<std::mutex> lock(up_mu);
-        if (!up_stream) HIP_TRY(hipStreamCreateWithFlags(&up_stream, hipStreamNonBlocking));
+        if (int st = upload_stream_locked()) return st;
         s = up_stream;
         return RLNC_OK;
     }
-    // host -> device copy of n bytes through the staging ring on the upload stream: returns once the bytes are in
-    // pinned memory (src may then be reused), the DMAs still queued; *slot = the ring slot of the last chunk
-    int upload(uint8_t *dst, const uint8_t *src, size_t n, int *slot) {
-        using rlnc::eng::kUpChunk;
-        hipStream_t s = nullptr;
-        if (int st = upload_stream(s)) return st;
+    int upload_flush_locked(rlnc::eng::UpSlot &u) {
+        if (!u.open) return RLNC_OK;
+        u.open = false;
+        for (const auto &r : u.runs)
+            HIP_TRY(hipMemcpyAsync(r.dst, u.buf.as<uint8_t>() + r.off, r.len, hipMemcpyHostToDevice, up_stream));
+        u.runs.clear();
+        HIP_TRY(hipEventRecord(u.ev, up_stream));
+        return RLNC_OK;
+    }
+    // host -> device copy of n bytes to dst through the staging ring: returns once the bytes are staged (src may then
+    // be reused).  pitch >= n: the destination row's size -- a piece landing right after the previous one's row
+    // joins its DMA (the pad bytes between rows are copied too).  *t = where the last byte was staged.
+    int upload(uint8_t *dst, const uint8_t *src, size_t n, size_t pitch, rlnc::eng::UpTicket *t) {
+        using namespace rlnc::eng;
+        std::lock_guard<std::mutex> lock(up_mu);
+        if (int st = upload_stream_locked()) return st;
         for (size_t o = 0; o < n; o += kUpChunk) {
             const size_t c = std::min(kUpChunk, n - o);
-            const int i = int(up_next.fetch_add(1, std::memory_order_relaxed) % rlnc::eng::kUpSlots);
-            rlnc::eng::UpSlot &u = up[i];
-            std::lock_guard<std::mutex> lock(u.mu);
-            if (!u.ev)
-                HIP_TRY(hipEventCreateWithFlags(&u.ev, hipEventDisableTiming));
+            const size_t span = (c == n && pitch <= kUpChunk) ? pitch : c;  // staged bytes incl. the row's pad
+            UpSlot *u = &up[up_cur];
+            if (!u->open || u->used + span > kUpChunk || u->runs.size() >= kUpRuns) {
+                if (int st = upload_flush_locked(*u)) return st;
+                up_cur = (up_cur + 1) % kUpSlots;
+                u = &up[up_cur];
+                if (!u->ev)
+                    HIP_TRY(hipEventCreateWithFlags(&u->ev, hipEventDisableTiming));
+                else
+                    HIP_TRY(hipEventSynchronize(u->ev));  // the slot's last flush has read it
+                if (int st = u->buf.ensure(kUpChunk)) return st;
+                u->used = 0;
+                u->gen += 1;
+                u->open = true;
+            }
+            std::memcpy(u->buf.as<uint8_t>() + u->used, src + o, c);
+            UpRun *last = u->runs.empty() ? nullptr : &u->runs.back();
+            if (last && last->dst + last->len == dst + o && last->off + last->len == u->used)
+                last->len += span;
             else
-                HIP_TRY(hipEventSynchronize(u.ev));  // the slot's previous DMA has read it
-            if (int st = u.buf.ensure(c)) return st;
-            std::memcpy(u.buf.p, src + o, c);
-            HIP_TRY(hipMemcpyAsync(dst + o, u.buf.p, c, hipMemcpyHostToDevice, s));
-            HIP_TRY(hipEventRecord(u.ev, s));
-            *slot = i;
+                u->runs.push_back(UpRun{dst + o, u->used, span});
+            u->used += span;
+            t->slot = up_cur;
+            t->gen = u->gen;
         }
         return RLNC_OK;
     }
-    // order stream s after every upload up to the one that used `slot` (see UpSlot)
-    int upload_wait(int slot, hipStream_t s) {
-        rlnc::eng::UpSlot &u = up[slot];
-        std::lock_guard<std::mutex> lock(u.mu);
-        HIP_TRY(hipStreamWaitEvent(s, u.ev, 0));
+    // flush the ticket's slot if it still holds the staged piece; *ev = nullptr when nothing was ever staged
+    int upload_flush(const rlnc::eng::UpTicket &t, hipEvent_t *ev) {
+        *ev = nullptr;
+        if (t.slot < 0) return RLNC_OK;
+        std::lock_guard<std::mutex> lock(up_mu);
+        rlnc::eng::UpSlot &u = up[t.slot];
+        if (u.gen == t.gen)
+            if (int st = upload_flush_locked(u)) return st;
+        *ev = u.ev;  // this flush, or a later one of the same slot (after it on the upload stream)
         return RLNC_OK;
     }
-    int upload_sync(int slot) {
-        rlnc::eng::UpSlot &u = up[slot];
-        std::lock_guard<std::mutex> lock(u.mu);
-        HIP_TRY(hipEventSynchronize(u.ev));
+    // order stream s after every upload up to the ticket's
+    int upload_wait(const rlnc::eng::UpTicket &t, hipStream_t s) {
+        hipEvent_t ev = nullptr;
+        if (int st = upload_flush(t, &ev)) return st;
+        if (!ev) return RLNC_OK;
+        std::lock_guard<std::mutex> lock(up_mu);  // the event is not re-recorded while waited on
+        HIP_TRY(hipStreamWaitEvent(s, ev, 0));
+        return RLNC_OK;
+    }
+    int upload_sync(const rlnc::eng::UpTicket &t) {
+        hipEvent_t ev = nullptr;
+        if (int st = upload_flush(t, &ev)) return st;
+        if (!ev) return RLNC_OK;
+        HIP_TRY(hipEventSynchronize(ev));
         return RLNC_OK;
     }
     // a call workspace, ordered after the work already enqueued on the context stream

@@ -75,14 +75,14 @@ struct rlnc_decoder {
     size_t store_slots = 0, store_cap = 0;
     // the context's upload-ring slot of the last upload into store (Decoder::decode returns once its piece is staged,
     // before the DMA): every later use of store, on whichever stream, is ordered after it
-    int up_slot = -1;
+    rlnc::eng::UpTicket up;
     void bind(rlnc_context *c) {
         ctx = c;
         c->retain();
     }
-    int order(hipStream_t s) const { return up_slot >= 0 ? ctx->upload_wait(up_slot, s) : RLNC_OK; }
+    int order(hipStream_t s) const { return ctx->upload_wait(up, s); }
     ~rlnc_decoder() {
-        if (up_slot >= 0) (void)ctx->upload_sync(up_slot);
+        (void)ctx->upload_sync(up);
         if (store) ctx->obj_free(store, store_cap);
         if (ctx) ctx->release();
     }
@@ -676,7 +676,7 @@ static int decoder_store_slot(rlnc_decoder *d, hipStream_t s, int slot, const ui
     if (kind == hipMemcpyHostToDevice)
         // staged through pinned memory: the caller may reuse the piece when the call returns, no synchronisation
         // (a pageable copy's cost 30 us per call for small pieces)
-        return d->ctx->upload(row, src, d->L, &d->up_slot);
+        return d->ctx->upload(row, src, d->L, d->stride, &d->up);
     HIP_TRY(hipMemcpyAsync(row, src, d->L, kind, s));
     HIP_TRY(hipStreamSynchronize(s));  // the caller may reuse the piece; the call is synchronous
     return RLNC_OK;

@@ -147,11 +147,12 @@ def test_clone_encoder_decoder_recoder(ctx, orc):
     assert np.array_equal(rec2.clone().recode(y), got)
 
 
-@pytest.mark.parametrize("data_len,k", [(1 << 20, 16), ((9 << 20) + 5, 2)])
+@pytest.mark.parametrize("data_len,k", [(1 << 20, 16), ((9 << 20) + 5, 2), (4_500_000, 64), (300_000, 200)])
 def test_decoder_staged_uploads(ctx, data_len, k):
     """Decoder::decode returns once its piece is staged in pinned memory, before the DMA: one caller buffer reused
-    for every piece, interleaved decoders cycling the staging ring, pieces over the 4 MiB chunk (several slots per
-    piece), a clone and a drop taken with uploads still in flight -- every decoded object equals its source."""
+    for every piece, interleaved decoders packing one staging slot and cycling the ring (the 4.5 MB / k = 64 case
+    wraps it several times), pieces over the 4 MiB slot (several slots per piece), a clone and a drop taken with
+    pieces still staged -- every decoded object equals its source."""
     from rlnc_amd.errors import RLNCError
     from rlnc_amd.full import Decoder, Encoder
 
