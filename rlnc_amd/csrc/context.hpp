@@ -74,12 +74,13 @@ struct DevBuf {
 struct PinBuf {
     void *p = nullptr;
     size_t cap = 0;
+    unsigned flags = hipHostMallocDefault;  // hipHostMallocCoherent: read / written by a running kernel
     int ensure(size_t bytes) {
         if (bytes <= cap) return RLNC_OK;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
-        HIP_TRY(hipHostMalloc(&p, std::max<size_t>(bytes, 256), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&p, std::max<size_t>(bytes, 256), flags));
         cap = std::max<size_t>(bytes, 256);
         return RLNC_OK;
     }
@@ -102,6 +103,13 @@ struct CallWs {
     hipEvent_t ev = nullptr;
     DevBuf coef, out, idx, scan, status, len;
     PinBuf pin_a, pin_b, pin_c;
+    // the call-latency kernel (piece.hip): coefficients read and output rows written by the kernel in host memory,
+    // per-chunk completion flags raised to the call's epoch, and the chunks' workgroup counters on the device
+    PinBuf pc_coef, pc_out, pc_flag;
+    DevBuf pc_count;
+    size_t pc_count_words = 0;  // zeroed words of pc_count
+    uint32_t epoch = 0;
+    CallWs() { pc_coef.flags = pc_out.flags = pc_flag.flags = hipHostMallocCoherent; }
     ~CallWs() {
         if (ev) (void)hipEventDestroy(ev);
         if (stream) (void)hipStreamDestroy(stream);
@@ -364,8 +372,9 @@ struct rlnc_context {
         HIP_TRY(hipEventSynchronize(ev));
         return RLNC_OK;
     }
-    // a call workspace, ordered after the work already enqueued on the context stream
-    int lease(std::unique_ptr<CallWs> &ws) {
+    // a call workspace; ordered: after the work already enqueued on the context stream (a call that reads
+    // memory the caller's stream-ordered work may still write, e.g. a borrowed device source)
+    int lease(std::unique_ptr<CallWs> &ws, bool ordered = true) {
         {
             std::lock_guard<std::mutex> lock(pool_mu);
             if (!pool.empty()) {
@@ -379,6 +388,7 @@ struct rlnc_context {
             HIP_TRY(hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&ws->ev, hipEventDisableTiming));
         }
+        if (!ordered) return RLNC_OK;
         HIP_TRY(hipEventRecord(ws->ev, stream));
         HIP_TRY(hipStreamWaitEvent(ws->stream, ws->ev, 0));
         return RLNC_OK;
@@ -423,7 +433,7 @@ struct Lease {
     rlnc_context *ctx;
     std::unique_ptr<CallWs> ws;
     explicit Lease(rlnc_context *c) : ctx(c) {}
-    int acquire() { return ctx->lease(ws); }
+    int acquire(bool ordered = true) { return ctx->lease(ws, ordered); }
     CallWs *operator->() const { return ws.get(); }
     ~Lease() { ctx->unlease(std::move(ws)); }
 };

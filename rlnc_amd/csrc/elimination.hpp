@@ -54,6 +54,7 @@ class Elimination {
     std::vector<uint8_t> m_;  // (k_ + 1) rows × stride()
     std::vector<uint8_t> live_;
     std::vector<uint8_t> used_;  // push's scratch: OR of the rows' E parts
+    std::vector<uint8_t> piv_, row_pad_;  // clean_backward's scratch: pivot flags, the row being scanned
 };
 
 }  // namespace rlnc

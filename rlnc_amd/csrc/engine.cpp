@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <cstdarg>
 #include <cstdio>
@@ -23,6 +24,7 @@
 #include "elimination.hpp"
 #include "gf256.hpp"
 #include "kernels.hpp"
+#include "piece.hpp"
 
 using rlnc::Elimination;
 using namespace rlnc::eng;
@@ -127,6 +129,90 @@ rlnc::MatmulParams encoder_params(const rlnc_encoder *e, const uint8_t *cv_dev, 
     p.width = int64_t(e->L);
     p.n_obj = 1;
     return p;
+}
+
+// ---- the call-latency path of the object API (piece.hip) ----------------------------------------------------------
+// Decoder::get_decoded_data takes it up to this much pinned staging and this many multiply-adds (the kernel reads
+// every source chunk once per output row, so larger products go to the batch kernels instead)
+constexpr size_t kPieceDecodeMaxBytes = size_t(64) << 20;
+constexpr size_t kPieceDecodeMaxMacs = size_t(1) << 31;
+
+// rows of `width` bytes at a 16-byte-aligned stride with room for the last slot's whole 16 bytes
+bool piece_eligible(const uint8_t *in, size_t in_row, size_t width) {
+    static const bool off = [] {
+        const char *e = getenv("RLNC_PIECE");  // A/B knob, read once: RLNC_PIECE=0 keeps the round-3 path
+        return e && atoi(e) == 0;
+    }();
+    return !off && (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (in_row & 15) == 0 && in_row >= round16(width);
+}
+
+int piece_waves_for(int n_in) {
+    static const int forced = [] {
+        const char *e = getenv("RLNC_PIECE_WAVES");  // A/B knob, read once
+        return e ? atoi(e) : 0;
+    }();
+    return forced ? forced : rlnc::piece_waves(n_in);
+}
+
+// Spin until the kernel raises *f to epoch.  The stream is queried only once the wait is long (a faulted kernel never
+// raises its flag: hipStreamQuery then reports the error).
+int piece_wait(const uint32_t *f, uint32_t epoch, hipStream_t s) {
+    if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == epoch) return RLNC_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; ++i) {
+        if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == epoch) return RLNC_OK;
+        __builtin_ia32_pause();
+        if ((i & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipErrorNotReady) continue;
+            if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == epoch) return RLNC_OK;
+            if (q == hipSuccess) return set_error(RLNC_ERR_DEVICE, "piece kernel finished without raising its flag");
+            return set_error(RLNC_ERR_DEVICE, "piece kernel: %s", hipGetErrorString(q));
+        }
+    }
+}
+
+// out rows r < n_out: dst[r·dst_row + 0 : width) = XOR_j ws->pc_coef[r·coef_row + j] · in[j·in_row + 0 : width), j < n_in
+// (the caller has written the coefficients into ws->pc_coef).  Synchronous: returns once dst holds every row.
+int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t width, size_t coef_row, size_t n_out,
+               uint8_t *dst, size_t dst_row) {
+    rlnc::PieceParams p{};
+    p.in = in;
+    p.in_row = int64_t(in_row);
+    p.coef = ws->pc_coef.as<uint8_t>();
+    p.coef_row = int64_t(coef_row);
+    p.out_row = int64_t(round16(width));
+    p.width = int64_t(width);
+    p.n_in = int(n_in);
+    p.n_out = int(n_out);
+    p.chunk_blocks = 64;  // 64 KiB of a row per completion flag: the host copies one while the device writes the next
+    const size_t chunks = size_t(rlnc::piece_chunks(p));
+    if (int st = ws->pc_out.ensure(n_out * size_t(p.out_row))) return st;
+    if (int st = ws->pc_flag.ensure(chunks * 4)) return st;
+    if (chunks > ws->pc_count_words) {
+        if (int st = ws->pc_count.ensure(chunks * 4)) return st;
+        HIP_TRY(hipMemsetAsync(ws->pc_count.p, 0, chunks * 4, ws->stream));
+        ws->pc_count_words = chunks;
+    }
+    p.out = ws->pc_out.as<uint8_t>();
+    p.count = ws->pc_count.as<uint32_t>();
+    p.flag = ws->pc_flag.as<uint32_t>();
+    if (++ws->epoch == 0) ws->epoch = 1;
+    p.epoch = ws->epoch;
+    HIP_TRY(rlnc::launch_piece(p, piece_waves_for(p.n_in), ws->stream));
+    const size_t chunk_bytes = size_t(p.chunk_blocks) * rlnc::kPieceCols;
+    const size_t cpr = chunks / n_out;
+    for (size_t c = 0; c < chunks; ++c) {
+        if (int st = piece_wait(p.flag + c, p.epoch, ws->stream)) {
+            // a failed launch may leave counters part-way: wait for the stream and re-arm them
+            (void)hipStreamSynchronize(ws->stream);
+            ws->pc_count_words = 0;
+            return st;
+        }
+        const size_t r = c / cpr, c0 = (c % cpr) * chunk_bytes, c1 = std::min(width, c0 + chunk_bytes);
+        std::memcpy(dst + r * dst_row + c0, p.out + r * size_t(p.out_row) + c0, c1 - c0);
+    }
+    return RLNC_OK;
 }
 
 }  // namespace
@@ -464,6 +550,13 @@ int rlnc_encoder_code_with_coding_vector(rlnc_encoder *e, const uint8_t *cv, siz
     int st = ctx->activate();
     if (st || (st = ctx->note_capture())) return st;
     Lease ws(ctx);
+    if (piece_eligible(e->src, e->stride, e->L)) {
+        // an owned source is immutable after Encoder::new (its upload synchronised); a borrowed one is ordered after
+        // the context stream's work
+        if ((st = ws.acquire(!e->owned)) || (st = ws->pc_coef.ensure(e->k))) return st;
+        std::memcpy(ws->pc_coef.p, cv, e->k);
+        return piece_call(ws.ws.get(), e->src, e->stride, e->k, e->L, e->k, 1, coded, e->L);
+    }
     if ((st = ws.acquire())) return st;
     if ((st = ws->coef.ensure(e->k)) || (st = ws->out.ensure(e->L))) return st;
     HIP_TRY(hipMemcpyAsync(ws->coef.p, cv, e->k, hipMemcpyHostToDevice, ws->stream));
@@ -583,6 +676,12 @@ int rlnc_recoder_recode_with_buf(rlnc_recoder *r, const uint8_t *rnd, size_t n_r
     int st = ctx->activate();
     if (st || (st = ctx->note_capture())) return st;
     Lease ws(ctx);
+    if (piece_eligible(r->pieces, r->stride, r->full)) {
+        // the received pieces are immutable after Recoder::new (its upload synchronised): no ordering
+        if ((st = ws.acquire(false)) || (st = ws->pc_coef.ensure(r->n))) return st;
+        std::memcpy(ws->pc_coef.p, rnd, r->n);
+        return piece_call(ws.ws.get(), r->pieces, r->stride, r->n, r->full, r->n, 1, full, r->full);
+    }
     if ((st = ws.acquire())) return st;
     if ((st = ws->coef.ensure(r->n)) || (st = ws->out.ensure(r->full))) return st;
     HIP_TRY(hipMemcpyAsync(ws->coef.p, rnd, r->n, hipMemcpyHostToDevice, ws->stream));
@@ -655,13 +754,19 @@ void rlnc_decoder_free(rlnc_decoder *d) { delete d; }
 
 // s: the stream of the row copy (host pieces: the context's upload stream, where a store reallocation then also runs)
 static int decoder_store_slot(rlnc_decoder *d, hipStream_t s, int slot, const uint8_t *src, hipMemcpyKind kind) {
-    if (int st = d->order(s)) return st;
+    // device pieces: the row copy on s follows the decoder's staged host uploads (a host piece's upload runs on the
+    // upload stream itself, behind every earlier one: no flush of the open ring slot per call)
+    if (kind != hipMemcpyHostToDevice)
+        if (int st = d->order(s)) return st;
     if (size_t(slot) >= d->store_slots) {
         const size_t ns = std::max(d->elim->slots(), size_t(slot) + 1);
         if (ns * d->stride > d->store_cap) {
             uint8_t *n = nullptr;
             size_t cap = 0;
             if (int st = d->ctx->obj_alloc(ns * d->stride, &n, &cap)) return st;
+            // staged rows still target the old store: flush them ahead of the copy
+            if (kind == hipMemcpyHostToDevice)
+                if (int st = d->order(s)) return st;
             if (d->store) {
                 HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, s));
                 HIP_TRY(hipStreamSynchronize(s));
@@ -730,6 +835,25 @@ size_t rlnc_decoder_get_received_piece_count(const rlnc_decoder *d) { return d ?
 size_t rlnc_decoder_get_useful_piece_count(const rlnc_decoder *d) { return d ? d->useful : 0; }
 size_t rlnc_decoder_get_remaining_piece_count(const rlnc_decoder *d) { return d ? d->k - d->useful : 0; }
 
+// the store holds (at least) `slots` rows, on stream s (after the decoder's uploads); rows never stored are zeroed
+// when `clear`
+static int decoder_store_rows(rlnc_decoder *d, hipStream_t s, size_t slots, bool clear) {
+    if (d->store_slots >= slots) return RLNC_OK;
+    if (slots * d->stride > d->store_cap) {
+        uint8_t *n = nullptr;
+        size_t cap = 0;
+        if (int st = d->ctx->obj_alloc(slots * d->stride, &n, &cap)) return st;
+        if (d->store) HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (d->store) d->ctx->obj_free(d->store, d->store_cap);
+        d->store = n;
+        d->store_cap = cap;
+    }
+    if (clear) HIP_TRY(hipMemsetAsync(d->store + d->store_slots * d->stride, 0, (slots - d->store_slots) * d->stride, s));
+    d->store_slots = slots;
+    return RLNC_OK;
+}
+
 // decoded rows = T × stored data rows, written to out_dev [k][L] on the lease's stream
 static int decoder_apply(rlnc_decoder *d, CallWs *ws, uint8_t *out_dev) {
     const size_t slots = d->elim->slots();
@@ -738,23 +862,8 @@ static int decoder_apply(rlnc_decoder *d, CallWs *ws, uint8_t *out_dev) {
     if ((st = ws->pin_b.ensure(d->k * slots)) || (st = ws->coef.ensure(d->k * slots))) return st;
     d->elim->transform(ws->pin_b.as<uint8_t>(), slots);
     HIP_TRY(hipMemcpyAsync(ws->coef.p, ws->pin_b.p, d->k * slots, hipMemcpyHostToDevice, ws->stream));
-    if (d->store_slots < slots) {
-        // slots never stored were never referenced; give them zero rows so T × D is well defined
-        if (slots * d->stride > d->store_cap) {
-            uint8_t *n = nullptr;
-            size_t cap = 0;
-            if ((st = d->ctx->obj_alloc(slots * d->stride, &n, &cap))) return st;
-            if (d->store)
-                HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, ws->stream));
-            HIP_TRY(hipStreamSynchronize(ws->stream));
-            if (d->store) d->ctx->obj_free(d->store, d->store_cap);
-            d->store = n;
-            d->store_cap = cap;
-        }
-        HIP_TRY(hipMemsetAsync(d->store + d->store_slots * d->stride, 0, (slots - d->store_slots) * d->stride,
-                               ws->stream));
-        d->store_slots = slots;
-    }
+    // slots never stored were never referenced; give them zero rows so T × D is well defined
+    if ((st = decoder_store_rows(d, ws->stream, slots, true))) return st;
     rlnc::MatmulParams p{};
     p.in = d->store;
     p.in_row = int64_t(d->stride);
@@ -776,10 +885,23 @@ int rlnc_decoder_get_decoded_data(rlnc_decoder *d, uint8_t *out, size_t cap, siz
     int st = d->ctx->activate();
     if (st) return st;
     Lease ws(d->ctx);
-    if ((st = ws.acquire()) || (st = ws->out.ensure(d->k * d->L))) return st;
-    if ((st = decoder_apply(d, ws.ws.get(), ws->out.as<uint8_t>()))) return st;
-    HIP_TRY(hipMemcpyAsync(out, ws->out.p, d->k * d->L, hipMemcpyDeviceToHost, ws->stream));
-    HIP_TRY(hipStreamSynchronize(ws->stream));
+    const size_t slots = d->elim->slots();
+    if (d->k * round16(d->L) <= kPieceDecodeMaxBytes && d->k * slots * d->L <= kPieceDecodeMaxMacs &&
+        piece_eligible(d->store, d->stride, d->L)) {
+        // T (k x slots) is read by the kernel from pinned memory and the rows land in pinned memory, copied into out
+        // chunk by chunk as the device finishes them.  Store rows never stored are referenced by zero columns of T
+        // only (0 · x = 0 for whatever they hold), so they need to exist, not to be cleared.
+        if ((st = ws.acquire(false)) || (st = d->order(ws->stream))) return st;
+        if ((st = decoder_store_rows(d, ws->stream, slots, false))) return st;
+        if ((st = ws->pc_coef.ensure(d->k * slots))) return st;
+        d->elim->transform(ws->pc_coef.as<uint8_t>(), slots);
+        if ((st = piece_call(ws.ws.get(), d->store, d->stride, slots, d->L, slots, d->k, out, d->L))) return st;
+    } else {
+        if ((st = ws.acquire()) || (st = ws->out.ensure(d->k * d->L))) return st;
+        if ((st = decoder_apply(d, ws.ws.get(), ws->out.as<uint8_t>()))) return st;
+        HIP_TRY(hipMemcpyAsync(out, ws->out.p, d->k * d->L, hipMemcpyDeviceToHost, ws->stream));
+        HIP_TRY(hipStreamSynchronize(ws->stream));
+    }
     // get_final_data_len — decoder.rs:162-177: last nonzero byte must be the 0x81 marker, not at 0
     size_t n = d->k * d->L;
     while (n > 0 && out[n - 1] == 0) --n;

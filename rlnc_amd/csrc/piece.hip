@@ -1,0 +1,174 @@
+// piece.hip — the object API's call-latency kernel: a few output rows, each out[r][0:width) =
+// XOR_j coef[r][j] · in[j][0:width) over GF(2^8), written straight into pinned host memory, with per-chunk
+// completion flags the host spins on while it copies finished chunks into the caller's buffer.
+//
+// Encoder::code_with_buf (encoder.rs:241-250), Recoder::recode_with_buf (recoder.rs:122-153) and the data side of
+// Decoder::get_decoded_data (decoder.rs:136-160) at the reference's small bench shapes (1 MB objects: one coded piece
+// is 4-64 KiB over 16-256 sources) cost the reference 11-22 us on one EPYC core.  A GPU call there is latency, not
+// bandwidth: the launch and completion round trip alone is 8-9 us on this box (scripts/ubench_call_latency.hip,
+// profiles/r04_call_latency.jsonl).  So this kernel
+//   * splits the sources (k) across the waves of a workgroup instead of walking them in one lane -- the GPU form of
+//     the reference's `parallel` split-then-XOR-reduce (encoder.rs:175-222): a workgroup owns 1 KiB of columns (16
+//     bytes a lane), each of its W waves multiplies ceil(k / W) source rows and the W partial sums meet in LDS;
+//   * reads the coefficients where the host left them (pinned memory: no H2D copy before the launch), one per lane,
+//     and turns each lane's coefficient into its 3-bit-split v_perm tables (kernels.hip) in registers; the wave then
+//     broadcasts row j's tables with v_readlane (no LDS table stage, no barrier before the arithmetic);
+//   * writes the output rows into pinned host memory (no D2H copy after it) with write-through stores and, per chunk
+//     of workgroups, counts finished workgroups in device memory; the chunk's last one raises its host flag, so the
+//     host copies chunk c into the caller's buffer while the device still writes chunk c + 1, and never calls
+//     hipStreamSynchronize (≈ 3 us of the round trip).  No release fence anywhere: a fence writes back the XCD's L2
+//     (1.7-6.5 us), per workgroup -- 1 MiB rows took 4x longer with one (profiles/r04_object_api_bench.txt).
+#include <hip/hip_runtime.h>
+
+#include "gf256.hpp"
+#include "piece.hpp"
+
+namespace rlnc {
+
+namespace {
+
+constexpr int kPF = 8;  // source rows in flight per lane
+constexpr int kSysWriteThrough = 17;  // buffer cache-policy bits sc0 | sc1: write-through to system scope
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+__device__ __forceinline__ uint32_t rl(uint32_t v, int lane) {
+    return uint32_t(__builtin_amdgcn_readlane(int(v), lane));
+}
+
+// make_perm_table (gf256.hpp) in registers: T0[v] = c·v is linear in the bits of v, so with m_b = c·2^b the
+// low dword's bytes are {0, m0, m1, m0^m1} and the high dword's are the low ones XOR m2 (likewise T1 from m3..m5,
+// T2 = {0, m6, m7, m6^m7})
+__device__ __forceinline__ void perm_table_regs(uint32_t c, uint32_t &t0lo, uint32_t &t0hi, uint32_t &t1lo,
+                                                uint32_t &t1hi, uint32_t &t2) {
+    uint32_t m[8];
+    m[0] = c;
+#pragma unroll
+    for (int b = 1; b < 8; ++b) m[b] = ((m[b - 1] << 1) ^ ((m[b - 1] & 0x80u) ? 0x1Bu : 0u)) & 0xFFu;
+    t0lo = (m[0] << 8) | (m[1] << 16) | ((m[0] ^ m[1]) << 24);
+    t0hi = t0lo ^ (m[2] * 0x01010101u);
+    t1lo = (m[3] << 8) | (m[4] << 16) | ((m[3] ^ m[4]) << 24);
+    t1hi = t1lo ^ (m[5] * 0x01010101u);
+    t2 = (m[6] << 8) | (m[7] << 16) | ((m[6] ^ m[7]) << 24);
+}
+
+// acc ^= c·x for the 16 bytes of x, c's tables t (wave-uniform)
+__device__ __forceinline__ void mac16(uint32_t (&acc)[4], const uint4 x, uint32_t t0lo, uint32_t t0hi, uint32_t t1lo,
+                                      uint32_t t1hi, uint32_t t2) {
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t s0 = w[q] & 0x07070707u, s1 = (w[q] >> 3) & 0x07070707u, s2 = (w[q] >> 6) & 0x03030303u;
+        acc[q] = xor3(xor3(acc[q], vperm(t0hi, t0lo, s0), vperm(t1hi, t1lo, s1)), vperm(t2, t2, s2), 0u);
+    }
+}
+
+// grid (ceil(width / kPieceCols), n_out); block 64·W threads (W = 1, 2, 4, 8 or 16 waves)
+__global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PieceParams p) {
+    __shared__ uint4 red[kPieceMaxWaves - 1][64];
+    const int W = int(blockDim.x) >> 6;
+    const int w = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
+    const int row = int(blockIdx.y);
+    const int R = (p.n_in + W - 1) / W;
+    const int r0 = min(p.n_in, w * R), r1 = min(p.n_in, r0 + R);
+    const int64_t col = int64_t(blockIdx.x) * kPieceCols + lane * 16;
+    const bool live = col < p.width;
+    // source rows are padded to 16 bytes (in_row >= round16(width)): the last slot loads whole.  Every load is
+    // unconditional from a valid address (lanes past the width read column 0, rows past the batch its last row), so
+    // the loads stay plain global loads with no per-lane select
+    const uint8_t *src = p.in + (live ? col : 0);
+    const uint8_t *coef = p.coef + int64_t(row) * p.coef_row;
+    uint32_t acc[4] = {0u, 0u, 0u, 0u};
+    for (int b0 = r0; b0 < r1; b0 += 64) {
+        const int nb = min(64, r1 - b0);
+        uint4 x[kPF];
+        // the first rows' loads go out before the coefficient read (a PCIe round trip when it sits in host memory)
+#pragma unroll
+        for (int u = 0; u < kPF; ++u) x[u] = *reinterpret_cast<const uint4 *>(src + int64_t(b0 + min(u, nb - 1)) * p.in_row);
+        uint32_t t0lo, t0hi, t1lo, t1hi, t2;
+        perm_table_regs(lane < nb ? coef[b0 + lane] : 0u, t0lo, t0hi, t1lo, t1hi, t2);
+        for (int j0 = 0; j0 < nb; j0 += kPF) {
+#pragma unroll
+            for (int u = 0; u < kPF; ++u) {
+                const int j = j0 + u;
+                if (j < nb) {  // wave-uniform
+                    const uint4 xv = x[u];
+                    if (j + kPF < nb) x[u] = *reinterpret_cast<const uint4 *>(src + int64_t(b0 + j + kPF) * p.in_row);
+                    mac16(acc, xv, rl(t0lo, j), rl(t0hi, j), rl(t1lo, j), rl(t1hi, j), rl(t2, j));
+                }
+            }
+        }
+    }
+    if (W > 1) {
+        if (w > 0) red[w - 1][lane] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+        __syncthreads();
+        if (w == 0)
+            for (int v = 0; v < W - 1; ++v) {
+                const uint4 o = red[v][lane];
+                acc[0] ^= o.x;
+                acc[1] ^= o.y;
+                acc[2] ^= o.z;
+                acc[3] ^= o.w;
+            }
+    }
+    // the output row is padded to 16 bytes too (out_row >= round16(width)): the last slot stores whole.  Stores are
+    // write-through to system scope (sc0 sc1), so no release fence (an L2 write-back per workgroup) is needed before
+    // the workgroup is counted: every storing wave drains its stores, the workgroup meets at a barrier, one lane adds
+    // to the chunk's counter (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms), and the chunk's last
+    // workgroup raises the host flag with a write-through store
+    if (w == 0 && live) {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(p.out + int64_t(row) * p.out_row, 0, 0x7FFFFFFF, 0x00020000);
+        const u32x4 v = {acc[0], acc[1], acc[2], acc[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, int(col), 0, kSysWriteThrough);
+    }
+    if (p.flag == nullptr) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int cpr = (int(gridDim.x) + p.chunk_blocks - 1) / p.chunk_blocks;  // chunks per row
+        const int cx = int(blockIdx.x) / p.chunk_blocks;
+        const int chunk = row * cpr + cx;
+        const unsigned in_chunk = unsigned(min(p.chunk_blocks, int(gridDim.x) - cx * p.chunk_blocks));
+        const unsigned prev = __hip_atomic_fetch_add(p.count + chunk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == in_chunk - 1) {
+            __hip_atomic_store(p.count + chunk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(p.flag + chunk, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+}  // namespace
+
+int piece_waves(int n_in) {
+    int w = 1;
+    while (w < n_in && w < kPieceMaxWaves) w <<= 1;
+    return w;
+}
+
+int piece_chunks(const PieceParams &p) {
+    const int64_t gx = (p.width + kPieceCols - 1) / kPieceCols;
+    return int((gx + p.chunk_blocks - 1) / p.chunk_blocks) * p.n_out;
+}
+
+hipError_t launch_piece(const PieceParams &p, int waves, hipStream_t s) {
+    const int64_t gx = (p.width + kPieceCols - 1) / kPieceCols;
+    if (p.n_in <= 0 || p.n_out <= 0 || p.n_out > 65535 || gx <= 0 || gx > 0x7FFFFFFFLL || p.chunk_blocks <= 0)
+        return hipErrorInvalidValue;
+    if (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16) return hipErrorInvalidValue;
+    if ((reinterpret_cast<uintptr_t>(p.in) | reinterpret_cast<uintptr_t>(p.out) | uintptr_t(p.in_row) |
+         uintptr_t(p.out_row)) & 15)
+        return hipErrorInvalidValue;
+    const int64_t padded = (p.width + 15) & ~int64_t(15);
+    if (padded > 0x7FFFFFF0LL) return hipErrorInvalidValue;  // 32-bit buffer offsets within a row
+    if (p.in_row < padded || (p.n_out > 1 && p.out_row < padded)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gf_piece_kernel, dim3(unsigned(gx), unsigned(p.n_out)), dim3(64 * waves), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace rlnc

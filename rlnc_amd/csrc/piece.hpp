@@ -1,0 +1,38 @@
+// piece.hpp — launch interface of the call-latency kernel in piece.hip (internal to librlnc_hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace rlnc {
+
+constexpr int kPieceCols = 1024;     // columns per workgroup (64 lanes x 16 bytes)
+constexpr int kPieceMaxWaves = 16;   // source-splitting waves per workgroup
+
+// out[r][0:width) = XOR_j coef[r][j] · in[j][0:width)  (r < n_out, j < n_in)
+// in, out, in_row, out_row 16-byte aligned; in_row (and out_row when n_out > 1) >= round16(width): the last 16-byte
+// slot of a row is read and written whole.  coef and out may be pinned host memory.
+// Completion (flag != nullptr): the grid's x blocks are cut into chunks of chunk_blocks workgroups per output row;
+// chunk c = row · chunks_per_row + x / chunk_blocks sets flag[c] = epoch (system scope) once all its workgroups'
+// stores are visible.  count: piece_chunks() device words, zero before the first launch (each chunk's last workgroup
+// zeroes its word again).
+struct PieceParams {
+    const uint8_t *in;
+    int64_t in_row;
+    const uint8_t *coef;
+    int64_t coef_row;
+    uint8_t *out;
+    int64_t out_row;
+    int64_t width;
+    int n_in, n_out;
+    uint32_t *count;
+    uint32_t *flag;
+    uint32_t epoch;
+    int chunk_blocks;
+};
+
+int piece_waves(int n_in);  // waves per workgroup: n_in rounded up to a power of two, at most kPieceMaxWaves
+int piece_chunks(const PieceParams &p);
+hipError_t launch_piece(const PieceParams &p, int waves, hipStream_t s);
+
+}  // namespace rlnc

@@ -103,3 +103,19 @@ def test_elimination_errors():
     with pytest.raises(RLNCError) as ei:
         Elimination(0)
     assert ei.value == RLNCError.PieceCountZero
+
+
+@pytest.mark.parametrize("k,sparsity,seed", [(64, 0.0, 1), (64, 0.9, 2), (130, 0.5, 3), (130, 0.97, 4),
+                                             (200, 0.0, 5), (200, 0.98, 6)])
+def test_large_k_sequences_match_oracle(k, sparsity, seed):
+    """The row-by-row backward pass and the last-row forward pass (elimination.cpp) across the 64-column scan blocks:
+    every status, the E rows' payload and the whole coefficient matrix equal the reference algorithm's."""
+    rng = np.random.default_rng(seed)
+    L = 6
+    pieces = _random_sequence(rng, k, L, k + k // 2, sparsity)
+    od = OracleDecoder(L, k)
+    want = [S[od.decode(p)] for p in pieces]
+    sts, payload, e = run_product(k, L, pieces, False)
+    assert sts == want
+    assert np.array_equal(payload, od.padded_payload())
+    assert np.array_equal(e.coefficients(), od.matrix()[:, :k])
