@@ -6,3 +6,4 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -3 gpurun_out/t1.log
 timeout -k 10 60 build/elim_push_bench > gpurun_out/elim_push.jsonl 2>&1
 timeout -k 10 200 build/object_api_bench --quick > gpurun_out/obj_piece.jsonl 2>&1
+timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err
