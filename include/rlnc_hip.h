@@ -85,7 +85,10 @@ int rlnc_context_device(const rlnc_context *ctx);
  * queue's unaligned memory mode, checked by a probe kernel when the first context on the device is created):
  * piece rows at any alignment (odd L from Encoder::new, data at byte k of a (k + L)-byte coded piece) then take the
  * vector kernels directly; 0: misaligned rows are copied through 16-byte-aligned scratch around them (same results).
- * -1 before a context exists on the device.  RLNC_ASSUME_ALIGNED_ONLY=1 in the environment forces 0. */
+ * -1 before a context exists on the device.  RLNC_ASSUME_ALIGNED_ONLY=1 in the environment forces 0 and skips the
+ * probe.  The probe's misaligned accesses return wrong bytes in the "dword" alignment mode (detected: 0) but fault
+ * the process under a strict alignment mode: on a queue configured that way (not the ROCm default for compute
+ * queues) set RLNC_ASSUME_ALIGNED_ONLY=1 before the first rlnc_context_create. */
 int rlnc_device_unaligned_vector_access(int device);
 
 /* ---- L1: vector primitives on device buffers (src/common/simd/mod.rs) --------------------------------

@@ -96,12 +96,24 @@ def stream_context(device: int, stream_handle: int) -> Context:
     if c is None:
         c = ctxs[key] = Context(device)
         c.set_stream(key[1])
+    else:
+        ctxs.move_to_end(key)
+    # closing a context synchronises its streams and frees its workspaces, which a graph capture in progress (torch's
+    # default global capture mode) forbids: evict at the next call outside a capture instead
+    if len(ctxs) > STREAM_CONTEXTS_PER_THREAD and not _capturing():
         evictable = [k for k, v in ctxs.items() if k != key and not v.graph_bound]
         while len(ctxs) > STREAM_CONTEXTS_PER_THREAD and evictable:
             ctxs.pop(evictable.pop(0)).close()
-    else:
-        ctxs.move_to_end(key)
     return c
+
+
+def _capturing() -> bool:
+    try:
+        import torch
+
+        return bool(torch.cuda.is_available() and torch.cuda.is_current_stream_capturing())
+    except Exception:
+        return False
 
 
 def release_stream_contexts() -> None:

@@ -136,6 +136,30 @@ struct UpSlot {
         if (ev) (void)hipEventDestroy(ev);
     }
 };
+// The stream-ordered uses of an object's device block (the *_batch_device calls, queued on whatever stream the
+// context had then): the block may be reused by another object only after the last of them.  Synchronous uses (the
+// object API on host buffers, the decoder's uploads) are complete when their call returns and need no record.
+struct ObjUse {
+    hipEvent_t ev = nullptr;  // recorded after the latest stream-ordered use
+    bool used = false;
+    bool captured = false;  // a use inside a HIP graph capture: the graph may replay it at any time
+    ~ObjUse() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    int note(hipStream_t s) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_TRY(hipStreamIsCapturing(s, &cs));
+        if (cs != hipStreamCaptureStatusNone) {
+            captured = true;
+            return RLNC_OK;
+        }
+        if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ev, s));
+        used = true;
+        return RLNC_OK;
+    }
+};
+
 constexpr int kUpSlots = 8;
 constexpr size_t kUpChunk = size_t(4) << 20;
 constexpr size_t kUpRuns = 256;  // runs per slot before it is flushed
@@ -249,7 +273,7 @@ struct rlnc_context {
         return b.ensure(bytes);
     }
     // an object's device block of at least n bytes (*cap = its size): a cached one when one fits (at most twice n
-    // plus 1 MiB), else hipMalloc
+    // plus 1 MiB), else hipMalloc -- after emptying the cache into the device if that fails
     int obj_alloc(size_t n, uint8_t **p, size_t *cap) {
         {
             std::lock_guard<std::mutex> lock(blk_mu);
@@ -267,17 +291,24 @@ struct rlnc_context {
             }
         }
         const size_t bytes = std::max<size_t>(n, 256);
-        HIP_TRY(hipMalloc(reinterpret_cast<void **>(p), bytes));
+        if (hipMalloc(reinterpret_cast<void **>(p), bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            {
+                std::lock_guard<std::mutex> lock(blk_mu);
+                for (auto &b : blk) (void)hipFree(b.second);
+                blk.clear();
+                blk_bytes = 0;
+            }
+            HIP_TRY(hipMalloc(reinterpret_cast<void **>(p), bytes));
+        }
         *cap = bytes;
         return RLNC_OK;
     }
-    // return an object's block (every upload into it already synchronised by the caller): the context stream's
-    // work (a _device call may still read it) is waited for, as hipFree would
-    void obj_free(void *p, size_t cap) {
+    // return an object's block: once its stream-ordered uses (u; nullptr = none) have run it joins the cache; a block
+    // a captured graph may still use is freed (hipFree waits for the device), as is a large one
+    void obj_free(void *p, size_t cap, const rlnc::eng::ObjUse *u) {
         if (!p) return;
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (cap > kBlkCacheBytes / 4 || hipStreamIsCapturing(stream, &cs) != hipSuccess ||
-            cs != hipStreamCaptureStatusNone || hipStreamSynchronize(stream) != hipSuccess) {
+        if (cap > kBlkCacheBytes / 4 || (u && u->captured) || (u && u->used && hipEventSynchronize(u->ev) != hipSuccess)) {
             (void)hipFree(p);
             return;
         }

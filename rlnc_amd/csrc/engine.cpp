@@ -43,12 +43,13 @@ struct rlnc_encoder {
     uint8_t *src = nullptr;  // k rows × stride
     size_t src_cap = 0;      // bytes of the owned block
     bool owned = false;
+    rlnc::eng::ObjUse use;   // code_batch_device launches reading src
     void bind(rlnc_context *c) {
         ctx = c;
         c->retain();
     }
     ~rlnc_encoder() {
-        if (owned && src) ctx->obj_free(src, src_cap);
+        if (owned && src) ctx->obj_free(src, src_cap, &use);
         if (ctx) ctx->release();
     }
 };
@@ -58,12 +59,13 @@ struct rlnc_recoder {
     size_t k = 0, n = 0, full = 0, stride = 0;
     uint8_t *pieces = nullptr;  // n rows × stride (coeffs ‖ data)
     size_t pieces_cap = 0;
+    rlnc::eng::ObjUse use;      // recode_batch_device launches reading pieces
     void bind(rlnc_context *c) {
         ctx = c;
         c->retain();
     }
     ~rlnc_recoder() {
-        if (pieces) ctx->obj_free(pieces, pieces_cap);
+        if (pieces) ctx->obj_free(pieces, pieces_cap, &use);
         if (ctx) ctx->release();
     }
 };
@@ -84,8 +86,9 @@ struct rlnc_decoder {
     }
     int order(hipStream_t s) const { return ctx->upload_wait(up, s); }
     ~rlnc_decoder() {
+        // every other use of the store is synchronous (decode_device, get_decoded_data*, clone): the uploads only
         (void)ctx->upload_sync(up);
-        if (store) ctx->obj_free(store, store_cap);
+        if (store) ctx->obj_free(store, store_cap, nullptr);
         if (ctx) ctx->release();
     }
 };
@@ -132,9 +135,11 @@ rlnc::MatmulParams encoder_params(const rlnc_encoder *e, const uint8_t *cv_dev, 
 }
 
 // ---- the call-latency path of the object API (piece.hip) ----------------------------------------------------------
-// Decoder::get_decoded_data takes it up to this much pinned staging and this many multiply-adds (the kernel reads
-// every source chunk once per output row, so larger products go to the batch kernels instead)
-constexpr size_t kPieceDecodeMaxBytes = size_t(64) << 20;
+// Decoder::get_decoded_data takes it up to this much output and this many multiply-adds (the kernel reads every
+// source chunk once per output row, so larger products go to the batch kernels instead; its 16-byte write-through
+// stores across PCIe run at ~10 GB/s, so outputs of many MiB come back faster as one DMA: 16 MiB objects 0.63 ms that
+// way against 0.92 through the kernel, 1 MiB objects 0.11 ms against 0.22 -- profiles/r04_object_api_bench_full_v1)
+constexpr size_t kPieceDecodeMaxBytes = size_t(4) << 20;
 constexpr size_t kPieceDecodeMaxMacs = size_t(1) << 31;
 
 // rows of `width` bytes at a 16-byte-aligned stride with room for the last slot's whole 16 bytes
@@ -172,20 +177,67 @@ int piece_wait(const uint32_t *f, uint32_t epoch, hipStream_t s) {
     }
 }
 
-// out rows r < n_out: dst[r·dst_row + 0 : width) = XOR_j ws->pc_coef[r·coef_row + j] · in[j·in_row + 0 : width), j < n_in
-// (the caller has written the coefficients into ws->pc_coef).  Synchronous: returns once dst holds every row.
-int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t width, size_t coef_row, size_t n_out,
-               uint8_t *dst, size_t dst_row) {
+// RLNC_PIECE_TRACE=1 (diagnostic, read once): per-phase host time of the piece calls, averaged, on stderr at exit
+struct PieceTrace {
+    bool on = [] {
+        const char *e = getenv("RLNC_PIECE_TRACE");
+        return e && atoi(e) != 0;
+    }();
+    std::atomic<uint64_t> calls{0}, ns_pre{0}, ns_launch{0}, ns_first{0}, ns_rest{0};
+    ~PieceTrace() {
+        const uint64_t n = calls.load();
+        if (on && n)
+            std::fprintf(stderr, "{\"piece_trace\": {\"calls\": %llu, \"pre_us\": %.2f, \"launch_us\": %.2f, "
+                                 "\"to_first_flag_us\": %.2f, \"copies_and_rest_us\": %.2f}}\n",
+                         (unsigned long long)n, ns_pre / 1e3 / n, ns_launch / 1e3 / n, ns_first / 1e3 / n,
+                         ns_rest / 1e3 / n);
+    }
+};
+PieceTrace g_piece_trace;
+inline uint64_t now_ns() {
+    return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                        std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+
+bool piece_inline() {
+    static const bool on = [] {
+        const char *e = getenv("RLNC_PIECE_INLINE");  // A/B knob, read once: 0 = coefficients always from pinned memory
+        return !e || atoi(e) != 0;
+    }();
+    return on;
+}
+
+int piece_chunk_blocks() {
+    static const int c = [] {
+        const char *e = getenv("RLNC_PIECE_CHUNK");  // A/B knob, read once: workgroups per completion flag
+        return e ? std::max(1, atoi(e)) : 64;
+    }();
+    return c;
+}
+
+// out rows r < n_out: dst[r·dst_row + 0 : width) = XOR_j coef[r·coef_row + j] · in[j·in_row + 0 : width), j < n_in.
+// coef: host memory; one row of at most kPieceInline bytes travels in the kernel arguments, more are read by the kernel
+// from ws->pc_coef (coef may already point there).  Synchronous: returns once dst holds every row.
+int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t width, const uint8_t *coef,
+               size_t coef_row, size_t n_out, uint8_t *dst, size_t dst_row) {
+    const uint64_t t0 = g_piece_trace.on ? now_ns() : 0;
     rlnc::PieceParams p{};
     p.in = in;
     p.in_row = int64_t(in_row);
-    p.coef = ws->pc_coef.as<uint8_t>();
     p.coef_row = int64_t(coef_row);
+    if (n_out == 1 && n_in <= size_t(rlnc::kPieceInline) && piece_inline()) {
+        p.coef = nullptr;
+        std::memcpy(p.coef_inline, coef, n_in);
+    } else {
+        if (int st = ws->pc_coef.ensure(n_out * coef_row)) return st;
+        if (coef != ws->pc_coef.as<uint8_t>()) std::memcpy(ws->pc_coef.p, coef, n_out * coef_row);
+        p.coef = ws->pc_coef.as<uint8_t>();
+    }
     p.out_row = int64_t(round16(width));
     p.width = int64_t(width);
     p.n_in = int(n_in);
     p.n_out = int(n_out);
-    p.chunk_blocks = 64;  // 64 KiB of a row per completion flag: the host copies one while the device writes the next
+    p.chunk_blocks = piece_chunk_blocks();  // 64 KiB of a row per flag: the host copies one while the device writes on
     const size_t chunks = size_t(rlnc::piece_chunks(p));
     if (int st = ws->pc_out.ensure(n_out * size_t(p.out_row))) return st;
     if (int st = ws->pc_flag.ensure(chunks * 4)) return st;
@@ -199,7 +251,10 @@ int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t
     p.flag = ws->pc_flag.as<uint32_t>();
     if (++ws->epoch == 0) ws->epoch = 1;
     p.epoch = ws->epoch;
+    const uint64_t t1 = g_piece_trace.on ? now_ns() : 0;
     HIP_TRY(rlnc::launch_piece(p, piece_waves_for(p.n_in), ws->stream));
+    const uint64_t t2 = g_piece_trace.on ? now_ns() : 0;
+    uint64_t t3 = 0;
     const size_t chunk_bytes = size_t(p.chunk_blocks) * rlnc::kPieceCols;
     const size_t cpr = chunks / n_out;
     for (size_t c = 0; c < chunks; ++c) {
@@ -209,8 +264,17 @@ int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t
             ws->pc_count_words = 0;
             return st;
         }
+        if (c == 0 && g_piece_trace.on) t3 = now_ns();
         const size_t r = c / cpr, c0 = (c % cpr) * chunk_bytes, c1 = std::min(width, c0 + chunk_bytes);
         std::memcpy(dst + r * dst_row + c0, p.out + r * size_t(p.out_row) + c0, c1 - c0);
+    }
+    if (g_piece_trace.on) {
+        const uint64_t t4 = now_ns();
+        g_piece_trace.calls += 1;
+        g_piece_trace.ns_pre += t1 - t0;
+        g_piece_trace.ns_launch += t2 - t1;
+        g_piece_trace.ns_first += t3 - t2;
+        g_piece_trace.ns_rest += t4 - t3;
     }
     return RLNC_OK;
 }
@@ -553,9 +617,8 @@ int rlnc_encoder_code_with_coding_vector(rlnc_encoder *e, const uint8_t *cv, siz
     if (piece_eligible(e->src, e->stride, e->L)) {
         // an owned source is immutable after Encoder::new (its upload synchronised); a borrowed one is ordered after
         // the context stream's work
-        if ((st = ws.acquire(!e->owned)) || (st = ws->pc_coef.ensure(e->k))) return st;
-        std::memcpy(ws->pc_coef.p, cv, e->k);
-        return piece_call(ws.ws.get(), e->src, e->stride, e->k, e->L, e->k, 1, coded, e->L);
+        if ((st = ws.acquire(!e->owned))) return st;
+        return piece_call(ws.ws.get(), e->src, e->stride, e->k, e->L, cv, e->k, 1, coded, e->L);
     }
     if ((st = ws.acquire())) return st;
     if ((st = ws->coef.ensure(e->k)) || (st = ws->out.ensure(e->L))) return st;
@@ -586,8 +649,10 @@ int rlnc_encoder_code_batch_device(rlnc_encoder *e, const uint8_t *coeffs_dev, s
     CHECK_ARG(row >= e->k + e->L);
     int st = e->ctx->activate();
     if (st || (st = e->ctx->note_capture())) return st;
-    return e->ctx->matmul(encoder_params(e, coeffs_dev, int64_t(e->k), int(n), out_dev + e->k, int64_t(row), out_dev,
-                                         int64_t(row)));
+    if ((st = e->ctx->matmul(encoder_params(e, coeffs_dev, int64_t(e->k), int(n), out_dev + e->k, int64_t(row), out_dev,
+                                            int64_t(row)))))
+        return st;
+    return e->owned ? e->use.note(e->ctx->stream) : RLNC_OK;
 }
 
 // ------------------------------------------------------------------------------------------------------
@@ -678,9 +743,8 @@ int rlnc_recoder_recode_with_buf(rlnc_recoder *r, const uint8_t *rnd, size_t n_r
     Lease ws(ctx);
     if (piece_eligible(r->pieces, r->stride, r->full)) {
         // the received pieces are immutable after Recoder::new (its upload synchronised): no ordering
-        if ((st = ws.acquire(false)) || (st = ws->pc_coef.ensure(r->n))) return st;
-        std::memcpy(ws->pc_coef.p, rnd, r->n);
-        return piece_call(ws.ws.get(), r->pieces, r->stride, r->n, r->full, r->n, 1, full, r->full);
+        if ((st = ws.acquire(false))) return st;
+        return piece_call(ws.ws.get(), r->pieces, r->stride, r->n, r->full, rnd, r->n, 1, full, r->full);
     }
     if ((st = ws.acquire())) return st;
     if ((st = ws->coef.ensure(r->n)) || (st = ws->out.ensure(r->full))) return st;
@@ -698,7 +762,8 @@ int rlnc_recoder_recode_batch_device(rlnc_recoder *r, const uint8_t *r_dev, size
     CHECK_ARG(r_dev != nullptr && out_dev != nullptr && count <= 0x7FFFFFFF);
     int st = r->ctx->activate();
     if (st || (st = r->ctx->note_capture())) return st;
-    return r->ctx->matmul(recoder_params(r, r_dev, int(count), out_dev, int64_t(r->full)));
+    if ((st = r->ctx->matmul(recoder_params(r, r_dev, int(count), out_dev, int64_t(r->full))))) return st;
+    return r->use.note(r->ctx->stream);
 }
 
 // ------------------------------------------------------------------------------------------------------
@@ -770,7 +835,7 @@ static int decoder_store_slot(rlnc_decoder *d, hipStream_t s, int slot, const ui
             if (d->store) {
                 HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, s));
                 HIP_TRY(hipStreamSynchronize(s));
-                d->ctx->obj_free(d->store, d->store_cap);
+                d->ctx->obj_free(d->store, d->store_cap, nullptr);
             }
             d->store = n;
             d->store_cap = cap;
@@ -845,7 +910,7 @@ static int decoder_store_rows(rlnc_decoder *d, hipStream_t s, size_t slots, bool
         if (int st = d->ctx->obj_alloc(slots * d->stride, &n, &cap)) return st;
         if (d->store) HIP_TRY(hipMemcpyAsync(n, d->store, d->store_slots * d->stride, hipMemcpyDeviceToDevice, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (d->store) d->ctx->obj_free(d->store, d->store_cap);
+        if (d->store) d->ctx->obj_free(d->store, d->store_cap, nullptr);
         d->store = n;
         d->store_cap = cap;
     }
@@ -895,7 +960,9 @@ int rlnc_decoder_get_decoded_data(rlnc_decoder *d, uint8_t *out, size_t cap, siz
         if ((st = decoder_store_rows(d, ws->stream, slots, false))) return st;
         if ((st = ws->pc_coef.ensure(d->k * slots))) return st;
         d->elim->transform(ws->pc_coef.as<uint8_t>(), slots);
-        if ((st = piece_call(ws.ws.get(), d->store, d->stride, slots, d->L, slots, d->k, out, d->L))) return st;
+        if ((st = piece_call(ws.ws.get(), d->store, d->stride, slots, d->L, ws->pc_coef.as<uint8_t>(), slots, d->k, out,
+                             d->L)))
+            return st;
     } else {
         if ((st = ws.acquire()) || (st = ws->out.ensure(d->k * d->L))) return st;
         if ((st = decoder_apply(d, ws.ws.get(), ws->out.as<uint8_t>()))) return st;

@@ -27,7 +27,7 @@ namespace rlnc {
 
 namespace {
 
-constexpr int kPF = 8;  // source rows in flight per lane
+constexpr int kPF = 16;  // source rows in flight per lane
 constexpr int kSysWriteThrough = 17;  // buffer cache-policy bits sc0 | sc1: write-through to system scope
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PiecePara
     // unconditional from a valid address (lanes past the width read column 0, rows past the batch its last row), so
     // the loads stay plain global loads with no per-lane select
     const uint8_t *src = p.in + (live ? col : 0);
-    const uint8_t *coef = p.coef + int64_t(row) * p.coef_row;
+    const uint8_t *coef = p.coef ? p.coef + int64_t(row) * p.coef_row : p.coef_inline;
     uint32_t acc[4] = {0u, 0u, 0u, 0u};
     for (int b0 = r0; b0 < r1; b0 += 64) {
         const int nb = min(64, r1 - b0);
@@ -130,6 +130,12 @@ __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PiecePara
     if (p.flag == nullptr) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (p.chunk_blocks == 1) {  // a flag per workgroup: no counter
+        if (threadIdx.x == 0)
+            __hip_atomic_store(p.flag + int64_t(row) * gridDim.x + blockIdx.x, p.epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     if (threadIdx.x == 0) {
         const int cpr = (int(gridDim.x) + p.chunk_blocks - 1) / p.chunk_blocks;  // chunks per row
         const int cx = int(blockIdx.x) / p.chunk_blocks;
@@ -145,11 +151,10 @@ __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PiecePara
 
 }  // namespace
 
-int piece_waves(int n_in) {
-    int w = 1;
-    while (w < n_in && w < kPieceMaxWaves) w <<= 1;
-    return w;
-}
+// rows per wave: 2-8 for up to 32 sources (4 waves), 8-16 for up to 128 (8 waves), 16 waves beyond -- the fastest of
+// 2/4/8/16 waves at each of the reference's 1 MB bench shapes (profiles/r04_piece_waves_ab.txt; one wave per source
+// measured 1-1.5 us slower at 16-64 sources: more waves to launch and to reduce)
+int piece_waves(int n_in) { return n_in <= 32 ? 4 : n_in <= 128 ? 8 : kPieceMaxWaves; }
 
 int piece_chunks(const PieceParams &p) {
     const int64_t gx = (p.width + kPieceCols - 1) / kPieceCols;
@@ -160,6 +165,7 @@ hipError_t launch_piece(const PieceParams &p, int waves, hipStream_t s) {
     const int64_t gx = (p.width + kPieceCols - 1) / kPieceCols;
     if (p.n_in <= 0 || p.n_out <= 0 || p.n_out > 65535 || gx <= 0 || gx > 0x7FFFFFFFLL || p.chunk_blocks <= 0)
         return hipErrorInvalidValue;
+    if (p.coef == nullptr && (p.n_out != 1 || p.n_in > kPieceInline)) return hipErrorInvalidValue;
     if (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16) return hipErrorInvalidValue;
     if ((reinterpret_cast<uintptr_t>(p.in) | reinterpret_cast<uintptr_t>(p.out) | uintptr_t(p.in_row) |
          uintptr_t(p.out_row)) & 15)

@@ -16,6 +16,8 @@ constexpr int kPieceMaxWaves = 16;   // source-splitting waves per workgroup
 // chunk c = row · chunks_per_row + x / chunk_blocks sets flag[c] = epoch (system scope) once all its workgroups'
 // stores are visible.  count: piece_chunks() device words, zero before the first launch (each chunk's last workgroup
 // zeroes its word again).
+constexpr int kPieceInline = 256;  // coefficient bytes carried in the kernel arguments (one output row, n_in <= this)
+
 struct PieceParams {
     const uint8_t *in;
     int64_t in_row;
@@ -29,9 +31,12 @@ struct PieceParams {
     uint32_t *flag;
     uint32_t epoch;
     int chunk_blocks;
+    // coef == nullptr: the coefficients are these bytes (n_out == 1): read from the kernel-argument segment in device
+    // memory instead of across PCIe from pinned host memory (a round trip at the head of every workgroup)
+    uint8_t coef_inline[kPieceInline];
 };
 
-int piece_waves(int n_in);  // waves per workgroup: n_in rounded up to a power of two, at most kPieceMaxWaves
+int piece_waves(int n_in);  // waves per workgroup for n_in sources
 int piece_chunks(const PieceParams &p);
 hipError_t launch_piece(const PieceParams &p, int waves, hipStream_t s);
 

@@ -81,6 +81,7 @@ int main(int argc, char **argv) {
     for (int a = 0; a < 15; ++a) {
         const Cfg c = kArgs[a];
         if (quick && c.bytes > (1u << 24)) continue;
+        if (std::getenv("OBJ_BENCH_SMALL") && c.bytes > (1u << 20)) continue;  // the 1 MB rows only
         std::vector<uint8_t> data(c.bytes);
         rng.fill_bytes(data.data(), data.size());
         Encoder enc = Encoder::create(data, c.k).unwrap();

@@ -1,0 +1,104 @@
+"""GPU: object lifetimes on a shared context (engine.cpp / context.hpp ObjUse).  Dropping an Encoder / Recoder /
+Decoder waits for that object's own stream-ordered uses only -- never for unrelated work queued on the context's
+stream -- and a dropped object's device block is reused by the next object only after every launch that read it,
+whichever stream the context used then."""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _long_batch(torch, ctx, reps):
+    """`reps` encode launches of 16 objects x k = 32 x 1 MiB x 32 coded pieces on the context's current stream:
+    ~0.6 ms each.  Returns the tensors (kept alive until the stream has run)."""
+    from rlnc_amd import batch
+
+    g = torch.Generator(device="cuda").manual_seed(1)
+    src = torch.randint(0, 256, (16, 32, 1 << 20), dtype=torch.uint8, device="cuda", generator=g)
+    co = torch.randint(0, 256, (16, 32, 32), dtype=torch.uint8, device="cuda", generator=g)
+    out = torch.empty((16, 32, 32 + (1 << 20)), dtype=torch.uint8, device="cuda")
+    for _ in range(reps):
+        batch.encode_batch(src, co, out, ctx)
+    return src, co, out
+
+
+def test_drop_does_not_wait_for_unrelated_stream_work():
+    """Objects built and used first (a decoder that decoded and returned its data, an encoder that also ran a
+    code_batch_device launch, a recoder); then ~100 ms of batch encodes queued on the context's stream; then the
+    objects are dropped: the drops return at once and the batch is still running after them.  (Round 3 synchronised
+    the whole context stream on every drop.)"""
+    import torch
+
+    import rlnc_amd
+    from rlnc_amd.full import Decoder, Encoder, Recoder
+
+    ctx = rlnc_amd.Context(0)
+    ctx.use_torch_stream()
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, 1 << 16, dtype=np.uint8)
+    enc = Encoder.new(data, 16, ctx)
+    pieces = [enc.code(rng) for _ in range(18)]
+    dec = Decoder.new(enc.get_piece_byte_len(), 16, ctx)
+    for p in pieces:
+        if dec.is_already_decoded():
+            break
+        try:
+            dec.decode(p)
+        except Exception:
+            pass
+    assert np.array_equal(dec.get_decoded_data(), data)
+    rec = Recoder.new(np.concatenate(pieces[:4]), enc.get_full_coded_piece_byte_len(), 16, ctx)
+    rec.recode(rng)
+    co = torch.from_numpy(rng.integers(0, 256, (4, 16), dtype=np.uint8)).cuda()
+    out = torch.empty((4, enc.get_full_coded_piece_byte_len()), dtype=torch.uint8, device="cuda")
+    enc.code_batch_device(co.data_ptr(), 4, out.data_ptr())
+    torch.cuda.synchronize()
+    keep = _long_batch(torch, ctx, 160)
+    t0 = time.perf_counter()
+    del dec, enc, rec
+    drop_ms = (time.perf_counter() - t0) * 1e3
+    still_running = not torch.cuda.current_stream().query()
+    torch.cuda.synchronize()
+    del keep
+    print(f"drops {drop_ms:.3f} ms, batch still running after them: {still_running}")
+    assert still_running, "the drops waited for the unrelated batch"
+    assert drop_ms < 5.0
+
+
+def test_dropped_encoder_block_reused_only_after_its_launches():
+    """code_batch_device queued on stream A (with unrelated work ahead of it), the context switched to stream B, the
+    encoder dropped, a new encoder of the same size built at once (the block cache hands it the old block; its upload
+    would overwrite the source): the launch on A still reads the old source (advisor round 3)."""
+    import torch
+
+    import rlnc_amd
+    from oracle.oracle import Oracle, build
+    from rlnc_amd.full import Encoder
+
+    build()
+    orc = Oracle()
+    ctx = rlnc_amd.Context(0)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    rng = np.random.default_rng(9)
+    k, L = 32, 1 << 16
+    data = rng.integers(0, 256, k * L, dtype=np.uint8)
+    enc = Encoder.without_padding(data, k, ctx)
+    n = 64
+    coeffs = rng.integers(0, 256, (n, k), dtype=np.uint8)
+    with torch.cuda.stream(sa):
+        co_dev = torch.from_numpy(coeffs).cuda()
+        out_dev = torch.zeros((n, k + L), dtype=torch.uint8, device="cuda")
+        ctx.use_torch_stream()
+        keep = _long_batch(torch, ctx, 60)  # ~40 ms ahead of the launch below on stream A
+        enc.code_batch_device(co_dev.data_ptr(), n, out_dev.data_ptr())
+    ctx.set_stream(sb.cuda_stream)
+    del enc
+    other = rng.integers(0, 256, k * L, dtype=np.uint8)
+    enc2 = Encoder.without_padding(other, k, ctx)  # same size: the cached block
+    sa.synchronize()
+    got = out_dev.cpu().numpy()
+    want = orc.encode(data.reshape(k, L), coeffs)
+    assert np.array_equal(got, want)
+    del enc2, keep
