@@ -1,0 +1,92 @@
+// bsj_tile.hpp — the tile body of the bit-sliced jump programs (the generated inline-asm programs of
+// bitslice_jump.inc, gen_bsjump.py): one workgroup's output rows x one 4 KiB column block.  Shared by the uniform and
+// ragged kernels of kernels.hip and the column-run A/B variant of kernels_ab.hip (internal to librlnc_hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "bitslice_jump.inc"
+#include "kernels.hpp"
+
+#ifndef RLNC_BSJ_SOFFSETS
+#error "bitslice_jump.inc must be generated with packed blocks (gen_bsjump.py default)"
+#endif
+
+namespace rlnc {
+namespace {
+
+constexpr int kBsjWaveRows = RLNC_BSJ_NT;  // output rows per wave; a workgroup of W waves = 8 W rows
+constexpr int kBsjColBlock = 4096;          // 64 lanes × 64 B, shared by the W waves
+
+// SHARE (W = 4 only): wave w builds one of the four combination sets of each source row and the sets are
+// exchanged through LDS (RLNC_BSJ_ASM_W4S) instead of every wave building all four
+// probe != nullptr (SHARE only): store the block table's address there and return (launch_bsj, once per device)
+// RUN (W = 8 only, variant 9): the workgroup walks `run` consecutive column blocks of one (object, row tile) --
+// the column-run program (RLNC_BSJ_ASM_W8R) carries the source-row stream across the tile boundaries, so only the
+// first tile pays the prologue (first DMAs, first sets); the grid is objects x row tiles x runs
+// The tile of one workgroup: output rows [rt * 8W, +8W) x column block cb of object obj (the uniform batch
+// kernel below and the ragged kernel both end here).
+template <int W, bool SHARE, bool RUN>
+__device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stream, int row_tiles, int rt, int cb,
+                                         int obj, uint32_t tiles, uint64_t *probe) {
+    constexpr int kTileRows = kBsjWaveRows * W;
+    // W = 8: one workgroup per CU, so a deeper ring and 2 BAR8 set slots (the builders run BAR8 rows ahead)
+    __shared__ __attribute__((aligned(16))) uint8_t ring[(W == 8 ? RLNC_BSJ_SLOTS8 : RLNC_BSJ_SLOTS) * kBsjColBlock];
+    __shared__ __attribute__((aligned(16))) uint8_t cset[SHARE ? (W == 8 ? RLNC_BSJ_CSET_BYTES8 : RLNC_BSJ_CSET_BYTES) : 16];
+    const int row0 = rt * kTileRows;
+    const int rows = min(kTileRows, p.n_out - row0);
+    if (p.hdr != nullptr && cb == 0) {  // coded-piece header (encoder.rs:246-248), 64·W threads
+        const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
+        uint8_t *h = p.hdr + int64_t(obj) * p.hdr_obj + int64_t(row0) * p.hdr_row;
+        for (int e = threadIdx.x; e < rows * p.n_in; e += 64 * W) {
+            const int i = e / p.n_in, j = e % p.n_in;
+            h[int64_t(i) * p.hdr_row + j] = coef_base[int64_t(i) * p.coef_row + j];
+        }
+    }
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const int rows_w = __builtin_amdgcn_readfirstlane(max(0, min(kBsjWaveRows, rows - kBsjWaveRows * w)));
+    const uint8_t *src = p.in + int64_t(obj) * p.in_obj + int64_t(cb) * kBsjColBlock;
+    uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0 + kBsjWaveRows * w) * p.out_row +
+                   int64_t(cb) * kBsjColBlock;
+    constexpr int kEntry = SHARE ? 8 : 4;  // bytes per stream entry: absolute address / block offset
+    const uint8_t *idx = static_cast<const uint8_t *>(stream) +
+                         ((int64_t(obj) * row_tiles + rt) * p.n_in * kTileRows + kBsjWaveRows * w) * kEntry;
+    typedef __attribute__((address_space(3))) uint8_t lds_u8;
+    const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)ring));  // addrspacecast
+    // W = 8 (shared): waves 0-3 stage the ring and build the sets exactly as in the 4-wave program, waves 4-7
+    // (cons = 1) only read the sets and call
+    constexpr int kStageWaves = (SHARE && W == 8) ? 4 : W;
+    const int ws = w % kStageWaves;
+    constexpr uint32_t kShare = kBsjColBlock / kStageWaves;  // bytes of each row a wave moves into the ring
+    const uint32_t ldsw = __builtin_amdgcn_readfirstlane(ring_lds + kShare * uint32_t(ws));
+    const uint32_t ldsr = ring_lds + 16u * lane;
+    const uint32_t dmaoff = kShare * uint32_t(ws) + 16u * lane;
+    const uint32_t off = 16u * lane;
+    const uint32_t ldsc = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)cset)) + 16u * lane;
+    const uint32_t ldscw = ldsc + 4096u * uint32_t(ws);      // this wave's set (group ws >> 1, half ws & 1)
+    const uint32_t ldsrg = ldsr + 2048u * uint32_t(ws >> 1);  // this wave's group of the ring chunk
+    const uint32_t half = uint32_t(ws & 1);
+    const uint32_t cons = uint32_t(w / kStageWaves);
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+#define RLNC_BSJ_OPERANDS                                                                                            \
+    : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),                           \
+      [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw), [off] "v"(off), \
+      [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr), [ldsc] "v"(ldsc), [ldscw] "v"(ldscw), [ldsrg] "v"(ldsrg),           \
+      [half] "s"(half), [probe] "s"(probe), [cons] "s"(cons), [ldsc2] "v"(ldsc + 65536u),                        \
+      [ldscw2] "v"(ldscw + 65536u), [tiles] "s"(tiles)                                                            \
+    : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S
+    if constexpr (W == 1) asm volatile(RLNC_BSJ_ASM_W1 : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 2) asm volatile(RLNC_BSJ_ASM_W2 : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 4 && !SHARE) asm volatile(RLNC_BSJ_ASM_W4 : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 4 && SHARE) asm volatile(RLNC_BSJ_ASM_W4S : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 8 && !RUN) asm volatile(RLNC_BSJ_ASM_W8S : RLNC_BSJ_OPERANDS);
+    if constexpr (W == 8 && RUN) asm volatile(RLNC_BSJ_ASM_W8R : RLNC_BSJ_OPERANDS);
+#undef RLNC_BSJ_OPERANDS
+#pragma clang diagnostic pop
+}
+
+}  // namespace
+}  // namespace rlnc

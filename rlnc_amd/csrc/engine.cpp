@@ -391,27 +391,21 @@ int rlnc_context_synchronize(rlnc_context *ctx) {
 }
 
 // Shipped decode paths: 0 auto, 1 host, 2 device, 5 device blocked run; 3, 4 and 6 (the round-1 LDS / register
-// forms) exist in diagnostic builds only (make -C rlnc_amd/csrc ab: -DRLNC_AB_VARIANTS).
+// forms) exist in the diagnostic build only (make -C rlnc_amd/csrc ab: rref_ab.hip).
 int rlnc_set_decode_path(rlnc_context *ctx, int path) {
-#ifdef RLNC_AB_VARIANTS
-    CHECK_ARG(ctx != nullptr && path >= 0 && path <= 6);
-#else
-    CHECK_ARG(ctx != nullptr && (path == 0 || path == 1 || path == 2 || path == 5));
-#endif
+    CHECK_ARG(ctx != nullptr && (path == 0 || path == 1 || path == 2 || path == 5 ||
+                                 (rlnc::ab_build() && (path == 3 || path == 4 || path == 6))));
     ctx->decode_path = path;
     return RLNC_OK;
 }
 
 int rlnc_set_kernel_variant(rlnc_context *ctx, int variant, int max_tile_rows) {
     CHECK_ARG(ctx != nullptr);
-#ifdef RLNC_AB_VARIANTS
-    CHECK_ARG(variant >= 0 && variant <= 9);
-#else
     // shipped: 0 perm, 1 nibble (the reference's tables, ablation), 6 (the unshared bit-sliced program, which also
     // serves <= 16-row products and a first use inside a graph capture), 7 and 8 (the bit-sliced default); 2-5 and 9
-    // are the A/B history, in diagnostic builds only
-    CHECK_ARG(variant == 0 || variant == 1 || variant == 6 || variant == 7 || variant == 8);
-#endif
+    // are the A/B history, in the diagnostic build only (kernels_ab.hip)
+    CHECK_ARG(variant == 0 || variant == 1 || variant == 6 || variant == 7 || variant == 8 ||
+              (rlnc::ab_build() && variant >= 2 && variant <= 9));
     CHECK_ARG(max_tile_rows == 0 || max_tile_rows == 1 || max_tile_rows == 2 || max_tile_rows == 4 ||
               max_tile_rows == 8 || max_tile_rows == 16 || max_tile_rows == 32);
     ctx->variant = static_cast<rlnc::MatmulVariant>(variant);

@@ -843,7 +843,8 @@ def main():
     ap.add_argument("--bar8", type=int, default=3, choices=(2, 3), help="8-wave program: a barrier every N rows")
     ap.add_argument("--prio8", default="off", help="K,L: 8-wave program's calls K.. of each row at s_setprio L")
     ap.add_argument("--no-m0step", action="store_true", help="shared programs: M0 moved as a literal per call")
-    ap.add_argument("--no-pack", action="store_true", help="shared programs: fixed-stride XOR3-only blocks")
+    ap.add_argument("--no-pack", action="store_true",
+                    help="shared programs: fixed-stride XOR3-only blocks (A/B history: bsj_tile.hpp requires packed)")
     ap.add_argument("--prio", default="", help="K,L: shared program's calls K.. of each row at s_setprio L")
     ap.add_argument("--load-hint", default="", help="cache-policy modifiers of the DMA loads, e.g. 'nt' (A/B)")
     ap.add_argument("--store-hint", default="", help="cache-policy modifiers of the tile stores, e.g. 'nt' (A/B)")

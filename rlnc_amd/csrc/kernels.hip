@@ -26,132 +26,13 @@
 
 #include "../../include/rlnc_hip.h"
 #include "gf256.hpp"
+#include "bsj_tile.hpp"
 #include "kernels.hpp"
+#include "kernels_common.hpp"
 
 namespace rlnc {
 
 namespace {
-
-constexpr int kThreads = 256;          // 4 waves
-constexpr int kBytesPerThread = 16;    // one dwordx4 per source row per lane
-constexpr int kColBlock = kThreads * kBytesPerThread;  // 4 KiB of columns per workgroup
-constexpr int kKC = 32;                // coefficient chunk (tables per chunk staged in LDS)
-
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-__device__ __forceinline__ uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel) {
-    return __builtin_amdgcn_perm(hi, lo, sel);
-}
-
-template <bool ALIGNED>
-__device__ __forceinline__ uint4 load16(const uint8_t *p, int nbytes) {
-    if (ALIGNED && nbytes == 16) return *reinterpret_cast<const uint4 *>(p);
-    uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int b = 0; b < 16; ++b)
-        if (b < nbytes) w[b >> 2] |= uint32_t(p[b]) << (8 * (b & 3));
-    return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-template <bool ALIGNED>
-__device__ __forceinline__ void store16(uint8_t *p, uint4 v, int nbytes) {
-    if (ALIGNED && nbytes == 16) {
-        *reinterpret_cast<uint4 *>(p) = v;
-        return;
-    }
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int b = 0; b < 16; ++b)
-        if (b < nbytes) p[b] = uint8_t(w[b >> 2] >> (8 * (b & 3)));
-}
-
-struct Sel {
-    uint32_t s0[4], s1[4], s2[4];
-};
-
-__device__ __forceinline__ Sel selectors(uint4 x) {
-    Sel s;
-    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        s.s0[q] = w[q] & 0x07070707u;
-        s.s1[q] = (w[q] >> 3) & 0x07070707u;
-        s.s2[q] = (w[q] >> 6) & 0x03030303u;
-    }
-    return s;
-}
-
-// XCD-aware work decode (cdna_hip_programming.md §5.5 T1): blocks b and b+8 share an XCD, so give every
-// XCD a contiguous range of work items, ordered row-tile-fastest: the row tiles of one column block then
-// run on one XCD and re-read that block's source rows from its L2 instead of HBM.
-__device__ __forceinline__ void decode_block(int total, int row_tiles, int col_blocks, int &rt, int &cb, int &obj) {
-    int b = blockIdx.x;
-    int w = b;
-    if ((total & 7) == 0) {
-        const int per = total >> 3;
-        w = (b & 7) * per + (b >> 3);
-    }
-    rt = w % row_tiles;
-    const int rest = w / row_tiles;
-    cb = rest % col_blocks;
-    obj = rest / col_blocks;
-}
-
-// Per-workgroup tile: column block cb of object obj, output rows [row0, row0 + rows_here).
-struct Tile {
-    int row0, rows_here, obj, cb;
-    int64_t col;
-    int nbytes;  // bytes of this lane's 16-byte column slot inside [0, width)
-};
-
-template <int NT>
-__device__ __forceinline__ Tile make_tile(const MatmulParams &p, int row_tiles, int col_blocks) {
-    Tile t;
-    int rt;
-    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, t.cb, t.obj);
-    t.row0 = rt * NT;
-    t.rows_here = min(NT, p.n_out - t.row0);
-    t.col = int64_t(t.cb) * kColBlock + int64_t(threadIdx.x) * kBytesPerThread;
-    t.nbytes = t.col < p.width ? int(min<int64_t>(kBytesPerThread, p.width - t.col)) : 0;
-    return t;
-}
-
-// VEC: plain 16-byte vector access (no per-lane branches in the hot loop, so the prefetched loads stay in
-// flight); otherwise byte-granular access bounded by nbytes (ragged tail / unaligned rows).
-template <bool VEC>
-__device__ __forceinline__ uint4 ld16(const uint8_t *p, int nbytes) {
-    if (VEC) return *reinterpret_cast<const uint4 *>(p);
-    return load16<false>(p, nbytes);
-}
-template <bool VEC>
-__device__ __forceinline__ void st16(uint8_t *p, uint4 v, int nbytes) {
-    if (VEC)
-        *reinterpret_cast<uint4 *>(p) = v;
-    else
-        store16<false>(p, v, nbytes);
-}
-
-template <int NT, bool VEC>
-__device__ __forceinline__ void store_tile(const MatmulParams &p, const Tile &t, const uint32_t (&acc)[NT][4]) {
-    if (!VEC && t.nbytes <= 0) return;
-    uint8_t *out_base = p.out + int64_t(t.obj) * p.out_obj + int64_t(t.row0) * p.out_row + t.col;
-#pragma unroll
-    for (int i = 0; i < NT; ++i)
-        if (i < t.rows_here)
-            st16<VEC>(out_base + int64_t(i) * p.out_row, make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]),
-                      t.nbytes);
-}
-
-__device__ __forceinline__ void copy_header(const MatmulParams &p, const Tile &t) {
-    if (p.hdr == nullptr || t.cb != 0) return;
-    const uint8_t *coef_base = p.coef + int64_t(t.obj) * p.coef_obj + int64_t(t.row0) * p.coef_row;
-    uint8_t *h = p.hdr + int64_t(t.obj) * p.hdr_obj + int64_t(t.row0) * p.hdr_row;
-    for (int e = threadIdx.x; e < t.rows_here * p.n_in; e += kThreads) {
-        const int i = e / p.n_in, j = e % p.n_in;
-        h[int64_t(i) * p.hdr_row + j] = coef_base[int64_t(i) * p.coef_row + j];
-    }
-}
 
 // main loop of the 2-source perm kernel over one coefficient chunk (tables already in LDS)
 template <int NT, bool VEC>
@@ -169,19 +50,10 @@ __device__ __forceinline__ void perm_chunk(const MatmulParams &p, const uint8_t 
         const Sel b = selectors(xb);
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
-#ifdef RLNC_DIAG_ONE_TABLE
-            // timing-only diagnostic build (wrong output): every row reuses row 0's tables, read once per
-            // row pair from LDS; the empty asm makes each row's copy opaque so no v_perm is CSE'd across rows
-            uint4 ta = s_t01[j][0], tb = s_t01[j + 1][0];
-            uint32_t ta2 = s_t2[j][0], tb2 = s_t2[j + 1][0];
-            asm volatile("" : "+v"(ta.x), "+v"(ta.y), "+v"(ta.z), "+v"(ta.w), "+v"(ta2));
-            asm volatile("" : "+v"(tb.x), "+v"(tb.y), "+v"(tb.z), "+v"(tb.w), "+v"(tb2));
-#else
             const uint4 ta = s_t01[j][i];
             const uint32_t ta2 = s_t2[j][i];
             const uint4 tb = s_t01[j + 1][i];  // zero table when j+1 == kc
             const uint32_t tb2 = s_t2[j + 1][i];
-#endif
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 uint32_t r = xor3(acc[i][q], vperm(ta.y, ta.x, a.s0[q]), vperm(ta.w, ta.z, a.s1[q]));
@@ -309,15 +181,9 @@ hipError_t launch_narrow(const MatmulParams &p, bool aligned, hipStream_t s) {
 // Streaming variant for few output rows (n_out <= 3: one coded piece per pass is HBM-bound, ~1 multiply-add
 // per source byte read): the perm kernel's arithmetic with PF source rows in flight per lane (it keeps one
 // row pair), loaded non-temporally (each source byte is read once).  Whole aligned 4 KiB blocks only.
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 ld16_nt(const uint8_t *ptr) {
-    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(ptr));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
 
-#ifndef RLNC_STREAM_FORM_DEFAULT
-#define RLNC_STREAM_FORM_DEFAULT 11  // stream3<PF 1, VW 2, 64-bit shifts>: profiles/r02_stream_ab.txt
-#endif
+constexpr int kStreamFormDefault = 11;  // stream3<PF 1, VW 2, 64-bit shifts>: profiles/r02_stream_ab.txt
+constexpr int kStreamPF = 2;            // rows in flight of gf_matmul_stream_kernel (2..16 A/B: r01_stream_pf_ab.txt)
 
 template <int NT, int PF>
 __global__ __launch_bounds__(kThreads) void gf_matmul_stream_kernel(MatmulParams p, int row_tiles, int col_blocks) {
@@ -352,11 +218,7 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_stream_kernel(MatmulParams
                 const int j = jb + u;
                 if (j >= kc) break;
                 const uint4 x = buf[u];
-#ifdef RLNC_STREAM_DRAIN  // A/B build: conditional prefetch (the compiler then drains all PF loads per group)
-                if (j + PF < kc) buf[u] = ld16_nt(rowp + int64_t(j + PF) * p.in_row);
-#else
                 buf[u] = ld16_nt(rowp + int64_t(min(j + PF, kc - 1)) * p.in_row);
-#endif
                 const Sel a = selectors(x);
 #pragma unroll
                 for (int i = 0; i < NT; ++i) {
@@ -374,30 +236,6 @@ __global__ __launch_bounds__(kThreads) void gf_matmul_stream_kernel(MatmulParams
     copy_header(p, t);
 }
 
-// Selectors from 64-bit shifts: one v_lshrrev_b64 shifts two dwords; the bits that cross the dword boundary land
-// in bits 29-31 (>> 3) or 26-31 (>> 6) of the low dword's top byte, which the masks clear.
-__device__ __forceinline__ Sel selectors64(uint4 x) {
-    Sel s;
-    const uint64_t a = (uint64_t(x.y) << 32) | x.x, b = (uint64_t(x.w) << 32) | x.z;
-    uint64_t a3, b3, a6, b6;  // the compiler splits a C++ 64-bit shift into 32-bit ones: ask for the pair form
-    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(a3) : "v"(a));
-    asm("v_lshrrev_b64 %0, 3, %1" : "=v"(b3) : "v"(b));
-    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(a6) : "v"(a));
-    asm("v_lshrrev_b64 %0, 6, %1" : "=v"(b6) : "v"(b));
-    s.s0[0] = x.x & 0x07070707u;
-    s.s0[1] = x.y & 0x07070707u;
-    s.s0[2] = x.z & 0x07070707u;
-    s.s0[3] = x.w & 0x07070707u;
-    s.s1[0] = uint32_t(a3) & 0x07070707u;
-    s.s1[1] = uint32_t(a3 >> 32) & 0x07070707u;
-    s.s1[2] = uint32_t(b3) & 0x07070707u;
-    s.s1[3] = uint32_t(b3 >> 32) & 0x07070707u;
-    s.s2[0] = uint32_t(a6) & 0x03030303u;
-    s.s2[1] = uint32_t(a6 >> 32) & 0x03030303u;
-    s.s2[2] = uint32_t(b6) & 0x03030303u;
-    s.s2[3] = uint32_t(b6 >> 32) & 0x03030303u;
-    return s;
-}
 
 // One-block streaming form with VW 16-byte slots per lane (slot v at column v * 4 KiB of a VW * 4 KiB block:
 // every table read feeds VW x the bytes, VW x PF loads in flight per lane) and optionally 64-bit-shift selectors.
@@ -550,12 +388,12 @@ int narrow_form() {
     return f;
 }
 
-// Single-pass stream kernel form; RLNC_STREAM_FORM (A/B knob, read once): 0 = gf_matmul_stream_kernel<NT, 2>,
-// 8..13 = gf_matmul_stream3_kernel forms (profiles/r02_stream_ab.txt)
+// Single-pass stream kernel form; RLNC_STREAM_FORM (A/B knob, read once): 11 = gf_matmul_stream3_kernel, 0 =
+// gf_matmul_stream_kernel<NT, 2> (the other measured forms: profiles/r02_stream_ab.txt, git history before round 4)
 int stream_form() {
     static const int f = [] {
         const char *e = getenv("RLNC_STREAM_FORM");
-        return e ? atoi(e) : RLNC_STREAM_FORM_DEFAULT;
+        return e ? atoi(e) : kStreamFormDefault;
     }();
     return f;
 }
@@ -577,242 +415,15 @@ hipError_t launch_stream(const MatmulParams &p, int64_t full, hipStream_t s, boo
             return launch_stream3<NT, 4, 1, true>(q, row_tiles, col_blocks, s, tail);
         switch (stream_form()) {
             case 11: return launch_stream3<NT, 1, 2, true>(q, row_tiles, col_blocks, s, tail);
-#ifdef RLNC_AB_VARIANTS  // the other measured forms (profiles/r02_stream_ab.txt), diagnostic builds only
-            case 8: return launch_stream3<NT, 2, 1, true>(q, row_tiles, col_blocks, s, tail);
-            case 9: return launch_stream3<NT, 2, 2, true>(q, row_tiles, col_blocks, s, tail);
-            case 10: return launch_stream3<NT, 2, 2, false>(q, row_tiles, col_blocks, s, tail);
-            case 12: return launch_stream3<NT, 3, 1, true>(q, row_tiles, col_blocks, s, tail);
-            case 13: return launch_stream3<NT, 2, 1, false>(q, row_tiles, col_blocks, s, tail);
-#endif
             default: tail_done = false; break;
         }
     }
     const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
     if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
-#ifndef RLNC_STREAM_PF
-#define RLNC_STREAM_PF 2  // A/B of 2..16 rows in flight: profiles/r01_stream_pf_ab.txt
-#endif
-    hipLaunchKernelGGL((gf_matmul_stream_kernel<NT, RLNC_STREAM_PF>), dim3(unsigned(total)), dim3(kThreads), 0, s, q,
+    hipLaunchKernelGGL((gf_matmul_stream_kernel<NT, kStreamPF>), dim3(unsigned(total)), dim3(kThreads), 0, s, q,
                        row_tiles, col_blocks);
     return hipGetLastError();
 }
-
-#ifdef RLNC_AB_VARIANTS  // variants 2-4 (perm3, wide2, wide4): A/B history, diagnostic builds only
-// Wide variant: each lane owns VW 16-byte slots per source row (slot v at column v·4 KiB inside an
-// (VW·4 KiB) block), so every table read from LDS — the measured bottleneck of the VW = 1 kernel (a build
-// that reads one table set per source row ran 2.2× faster) — feeds VW× more multiply-adds.  Full aligned
-// blocks only; ragged tails go to the VW = 1 kernels.
-template <int NT, int VW>
-__global__ __launch_bounds__(kThreads) void gf_matmul_wide_kernel(MatmulParams p, int row_tiles, int col_blocks) {
-    __shared__ uint4 s_t01[kKC][NT];
-    __shared__ uint32_t s_t2[kKC][NT];
-    constexpr int64_t kSlot = int64_t(kThreads) * kBytesPerThread;  // 4 KiB between a lane's slots
-
-    int rt, cb, obj;
-    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
-    const int row0 = rt * NT;
-    const int rows_here = min(NT, p.n_out - row0);
-    const int64_t col = int64_t(cb) * kSlot * VW + int64_t(threadIdx.x) * kBytesPerThread;
-    const uint8_t *in_base = p.in + int64_t(obj) * p.in_obj + col;
-    const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
-
-    uint32_t acc[NT][VW][4];
-#pragma unroll
-    for (int i = 0; i < NT; ++i)
-#pragma unroll
-        for (int v = 0; v < VW; ++v) acc[i][v][0] = acc[i][v][1] = acc[i][v][2] = acc[i][v][3] = 0u;
-
-    for (int j0 = 0; j0 < p.n_in; j0 += kKC) {
-        const int kc = min(kKC, p.n_in - j0);
-        if (j0) __syncthreads();
-        for (int e = threadIdx.x; e < kKC * NT; e += kThreads) {
-            const int i = e % NT, j = e / NT;
-            const uint8_t c = (i < rows_here && j < kc) ? coef_base[int64_t(i) * p.coef_row + j0 + j] : uint8_t(0);
-            const PermTable pt = make_perm_table(c);
-            s_t01[j][i] = make_uint4(pt.t0lo, pt.t0hi, pt.t1lo, pt.t1hi);
-            s_t2[j][i] = pt.t2;
-        }
-        __syncthreads();
-        const uint8_t *rowp = in_base + int64_t(j0) * p.in_row;
-        const uint4 zero = make_uint4(0, 0, 0, 0);
-        uint4 na[VW], nb[VW];
-#pragma unroll
-        for (int v = 0; v < VW; ++v) {
-            na[v] = *reinterpret_cast<const uint4 *>(rowp + v * kSlot);
-            nb[v] = kc > 1 ? *reinterpret_cast<const uint4 *>(rowp + p.in_row + v * kSlot) : zero;
-        }
-        for (int j = 0; j < kc; j += 2) {
-            Sel a[VW], b[VW];
-#pragma unroll
-            for (int v = 0; v < VW; ++v) {
-                a[v] = selectors(na[v]);
-                b[v] = selectors(nb[v]);
-            }
-            // prefetch the next row pair while this pair is multiplied
-#pragma unroll
-            for (int v = 0; v < VW; ++v) {
-                if (j + 2 < kc) na[v] = *reinterpret_cast<const uint4 *>(rowp + int64_t(j + 2) * p.in_row + v * kSlot);
-                nb[v] = (j + 3 < kc) ? *reinterpret_cast<const uint4 *>(rowp + int64_t(j + 3) * p.in_row + v * kSlot) : zero;
-            }
-#pragma unroll
-            for (int i = 0; i < NT; ++i) {
-                const uint4 ta = s_t01[j][i];
-                const uint32_t ta2 = s_t2[j][i];
-                const uint4 tb = s_t01[j + 1][i];
-                const uint32_t tb2 = s_t2[j + 1][i];
-#pragma unroll
-                for (int v = 0; v < VW; ++v)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        uint32_t r = xor3(acc[i][v][q], vperm(ta.y, ta.x, a[v].s0[q]), vperm(ta.w, ta.z, a[v].s1[q]));
-                        r = xor3(r, vperm(ta2, ta2, a[v].s2[q]), vperm(tb.y, tb.x, b[v].s0[q]));
-                        acc[i][v][q] = xor3(r, vperm(tb.w, tb.z, b[v].s1[q]), vperm(tb2, tb2, b[v].s2[q]));
-                    }
-            }
-        }
-    }
-    uint8_t *out_base = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + col;
-#pragma unroll
-    for (int i = 0; i < NT; ++i)
-        if (i < rows_here)
-#pragma unroll
-            for (int v = 0; v < VW; ++v)
-                *reinterpret_cast<uint4 *>(out_base + int64_t(i) * p.out_row + v * kSlot) =
-                    make_uint4(acc[i][v][0], acc[i][v][1], acc[i][v][2], acc[i][v][3]);
-    if (p.hdr != nullptr && cb == 0) {
-        uint8_t *h = p.hdr + int64_t(obj) * p.hdr_obj + int64_t(row0) * p.hdr_row;
-        for (int e = threadIdx.x; e < rows_here * p.n_in; e += kThreads) {
-            const int i = e / p.n_in, j = e % p.n_in;
-            h[int64_t(i) * p.hdr_row + j] = coef_base[int64_t(i) * p.coef_row + j];
-        }
-    }
-}
-
-// Three-source variant: the 24 bits of three source bytes (x, y, z) are cut into eight 3-bit chunks
-//   x0-2 | x3-5 | x6,x7,y0 | y1-3 | y4-6 | y7,z0,z1 | z2-4 | z5-7
-// and each chunk indexes an 8-entry table that already sums the contributions of the coefficients it
-// straddles, so three multiply-accumulates of a word cost 8 v_perm_b32 + 4 v_bitop3_b32 (4.0 VALU ops per
-// word-multiply-add instead of 4.5).  XOR is associative and GF(2^8) products are exact, so the result is
-// byte-identical to the reference's sequential dst ^= c_j · src_j loop.
-constexpr int kKC3 = 33;  // coefficient chunk: 11 triples
-
-__device__ __forceinline__ void triple_tables(uint8_t cx, uint8_t cy, uint8_t cz, uint4 out[4]) {
-    uint8_t b[24];  // basis: b[t] = contribution of bit t of the 24-bit chunk stream
-    uint8_t mx = cx, my = cy, mz = cz;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-        b[t] = mx;
-        b[8 + t] = my;
-        b[16 + t] = mz;
-        mx = gf_xtime(mx);
-        my = gf_xtime(my);
-        mz = gf_xtime(mz);
-    }
-    uint32_t w[16];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        uint32_t lo = 0, hi = 0;
-#pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            uint8_t e = 0;
-#pragma unroll
-            for (int t = 0; t < 3; ++t)
-                if (v & (1 << t)) e ^= b[3 * c + t];
-            if (v < 4)
-                lo |= uint32_t(e) << (8 * v);
-            else
-                hi |= uint32_t(e) << (8 * (v - 4));
-        }
-        w[2 * c] = lo;
-        w[2 * c + 1] = hi;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) out[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-}
-
-struct Sel3 {
-    uint32_t s[8][4];
-};
-
-__device__ __forceinline__ Sel3 selectors3(uint4 X, uint4 Y, uint4 Z) {
-    Sel3 r;
-    const uint32_t xs[4] = {X.x, X.y, X.z, X.w}, ys[4] = {Y.x, Y.y, Y.z, Y.w}, zs[4] = {Z.x, Z.y, Z.z, Z.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t x = xs[q], y = ys[q], z = zs[q];
-        r.s[0][q] = x & 0x07070707u;
-        r.s[1][q] = (x >> 3) & 0x07070707u;
-        r.s[2][q] = ((x >> 6) & 0x03030303u) | ((y << 2) & 0x04040404u);
-        r.s[3][q] = (y >> 1) & 0x07070707u;
-        r.s[4][q] = (y >> 4) & 0x07070707u;
-        r.s[5][q] = ((y >> 7) & 0x01010101u) | ((z << 1) & 0x06060606u);
-        r.s[6][q] = (z >> 2) & 0x07070707u;
-        r.s[7][q] = (z >> 5) & 0x07070707u;
-    }
-    return r;
-}
-
-template <int NT, bool VEC>
-__device__ __forceinline__ void perm3_chunk(const MatmulParams &p, const uint8_t *rowp, int kc, int nbytes,
-                                            const uint4 (*s_tab)[NT][4], uint32_t (&acc)[NT][4]) {
-    const uint4 zero = make_uint4(0, 0, 0, 0);
-    const int kt = (kc + 2) / 3;
-    auto ld = [&](int j) { return j < kc ? ld16<VEC>(rowp + int64_t(j) * p.in_row, nbytes) : zero; };
-    uint4 nx = ld(0), ny = ld(1), nz = ld(2);
-    for (int t = 0; t < kt; ++t) {
-        const Sel3 s = selectors3(nx, ny, nz);
-        // prefetch the next triple of source rows while this one is multiplied
-        nx = ld(3 * t + 3);
-        ny = ld(3 * t + 4);
-        nz = ld(3 * t + 5);
-#pragma unroll
-        for (int i = 0; i < NT; ++i) {
-            const uint4 a = s_tab[t][i][0], b = s_tab[t][i][1], c = s_tab[t][i][2], d = s_tab[t][i][3];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t u0 = xor3(vperm(a.y, a.x, s.s[0][q]), vperm(a.w, a.z, s.s[1][q]), vperm(b.y, b.x, s.s[2][q]));
-                const uint32_t u1 = xor3(vperm(b.w, b.z, s.s[3][q]), vperm(c.y, c.x, s.s[4][q]), vperm(c.w, c.z, s.s[5][q]));
-                const uint32_t u2 = xor3(vperm(d.y, d.x, s.s[6][q]), vperm(d.w, d.z, s.s[7][q]), acc[i][q]);
-                acc[i][q] = xor3(u0, u1, u2);
-            }
-        }
-    }
-}
-
-// VEC: every lane owns a full, aligned 16-byte slot (all blocks but a ragged/unaligned tail)
-template <int NT, bool VEC>
-__global__ __launch_bounds__(kThreads) void gf_matmul_perm3_kernel(MatmulParams p, int row_tiles, int col_blocks) {
-    constexpr int KT = kKC3 / 3;
-    __shared__ uint4 s_tab[KT][NT][4];
-
-    const Tile t = make_tile<NT>(p, row_tiles, col_blocks);
-    const uint8_t *in_base = p.in + int64_t(t.obj) * p.in_obj + t.col;
-    const uint8_t *coef_base = p.coef + int64_t(t.obj) * p.coef_obj + int64_t(t.row0) * p.coef_row;
-
-    uint32_t acc[NT][4];
-#pragma unroll
-    for (int i = 0; i < NT; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0u;
-
-    for (int j0 = 0; j0 < p.n_in; j0 += kKC3) {
-        const int kc = min(kKC3, p.n_in - j0);
-        if (j0) __syncthreads();
-        for (int e = threadIdx.x; e < KT * NT; e += kThreads) {
-            const int i = e % NT, tt = e / NT;
-            uint8_t c3[3] = {0, 0, 0};
-            if (i < t.rows_here)
-                for (int u = 0; u < 3; ++u)
-                    if (3 * tt + u < kc) c3[u] = coef_base[int64_t(i) * p.coef_row + j0 + 3 * tt + u];
-            triple_tables(c3[0], c3[1], c3[2], s_tab[tt][i]);
-        }
-        __syncthreads();
-        if (VEC || t.nbytes > 0)
-            perm3_chunk<NT, VEC>(p, in_base + int64_t(j0) * p.in_row, kc, t.nbytes, s_tab, acc);
-    }
-    store_tile<NT, VEC>(p, t, acc);
-    copy_header(p, t);
-}
-
-#endif  // RLNC_AB_VARIANTS
 
 // Ablation baseline: the reference's 4-bit split (LOW/HIGH nibble tables, simd_mul_table.rs:36-80) in
 // LDS, one ds_read_u8 per nibble per byte per lane.
@@ -891,11 +502,6 @@ hipError_t launch_one(const MatmulParams &p, int64_t width, hipStream_t s, Matmu
     MatmulParams q = p;
     q.width = width;
     const dim3 grid{unsigned(total)}, block{unsigned(kThreads)};
-#ifdef RLNC_AB_VARIANTS
-    if (v == MatmulVariant::Perm3)
-        hipLaunchKernelGGL((gf_matmul_perm3_kernel<NT, VEC>), grid, block, 0, s, q, row_tiles, col_blocks);
-    else
-#endif
     if (v == MatmulVariant::NibbleLds)
         hipLaunchKernelGGL((gf_matmul_nibble_kernel<NT, VEC>), grid, block, 0, s, q, row_tiles, col_blocks);
     else
@@ -921,179 +527,18 @@ hipError_t launch_nt(const MatmulParams &p, hipStream_t s, MatmulVariant v, bool
     return launch_one<NT, false>(t, p.width - full, s, v);
 }
 
-#ifdef RLNC_AB_VARIANTS
-template <int NT, int VW>
-hipError_t launch_wide(const MatmulParams &p, int64_t full, hipStream_t s) {
-    const int row_tiles = (p.n_out + NT - 1) / NT;
-    const int col_blocks = int(full / (int64_t(kColBlock) * VW));
-    const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
-    if (total <= 0) return hipSuccess;
-    if (total > 0x7FFFFFFFLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((gf_matmul_wide_kernel<NT, VW>), dim3(unsigned(total)), dim3(kThreads), 0, s, p, row_tiles,
-                       col_blocks);
-    return hipGetLastError();
-}
-
-template <int NT>
-hipError_t launch_nt(const MatmulParams &p, hipStream_t s, MatmulVariant v, bool aligned);
-
-// Wide variant: whole (VW·4 KiB) blocks through gf_matmul_wide_kernel, the rest through the VW = 1 path.
-template <int NT, int VW>
-hipError_t launch_wide_split(const MatmulParams &p, hipStream_t s) {
-    const int64_t blk = int64_t(kColBlock) * VW;
-    const int64_t full = (p.width / blk) * blk;
-    if (full > 0) {
-        hipError_t e = launch_wide<NT, VW>(p, full, s);
-        if (e != hipSuccess) return e;
-    }
-    if (full == p.width) return hipSuccess;
-    MatmulParams t = p;
-    t.in = p.in + full;
-    t.out = p.out + full;
-    t.width = p.width - full;
-    if (full > 0) t.hdr = nullptr;
-    return launch_nt<NT>(t, s, MatmulVariant::Perm, true);
-}
-
-#endif  // RLNC_AB_VARIANTS
-
-inline bool al16(const void *ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
-inline bool al16(int64_t v) { return (v & 15) == 0; }
-
-#ifdef RLNC_AB_VARIANTS  // variant 5 (register-indexed XORs): A/B history, diagnostic builds only
-// ---------------------------------------------------------------------------------------------------
-// Bit-sliced variant (gen_bitslice.py has the full derivation).  Measured on gfx950: v_perm_b32 issues at
-// ~4.1 cycles/wave64, so the 3-perm lookup costs ~19 cycles per 32-bit multiply-add; GF(2^8) multiply by
-// c is instead a GF(2)-linear map on bit-planes, applied with 16 register-indexed XORs per 32 bytes per
-// group, the index pair shared by two groups (s_set_gpr_idx_idx + 2 v_xor_b32, ~2 cycles per XOR), i.e.
-// ~8 cycles of issue per 32 bytes·source·row plus the amortised transposes.
-// ---------------------------------------------------------------------------------------------------
-#ifdef RLNC_BS_ASM_FILE  // diagnostic builds (scripts/bs_diag.sh) substitute a generated variant
-#include RLNC_BS_ASM_FILE
-#else
-#include "bitslice_asm.inc"
-#endif
-
-constexpr int kBsRows = RLNC_BS_NT;           // output rows per workgroup
-constexpr int kBsColBlock = 16384;            // 256 lanes × 64 B
-constexpr int kBsRowDwords = RLNC_BS_ROW_DWORDS;  // packed indices per (row, source)
-
-// Index n = 2·o + h of (row, source) says which of the source's planes 4h..4h+3 feed output plane o: bit b
-// of idx = bit o of (c · 2^(4h+b)).  Packed three per dword as bytes 0x10 | idx, byte 3 = 0x10 (see
-// gen_bitslice.py: the byte above each index supplies M0[15:12], the relative-SRC0 enable).  Stream order
-// [obj][row tile][j][row in tile][6 dwords] is the order the main kernel consumes it; rows past n_out get
-// c = 0 (all indices 0: XOR of the zero register).
-__global__ __launch_bounds__(64) void bs_index_kernel(const uint8_t *coef, int64_t coef_obj, int64_t coef_row,
-                                                      int n_out, int n_in, int row_tiles, uint32_t *stream) {
-    const int j = blockIdx.x, rt = blockIdx.y, obj = blockIdx.z;
-    const int i = threadIdx.x / kBsRowDwords, d = threadIdx.x % kBsRowDwords;
-    if (i >= kBsRows) return;
-    const int row = rt * kBsRows + i;
-    const uint32_t c = row < n_out ? coef[int64_t(obj) * coef_obj + int64_t(row) * coef_row + j] : 0u;
-    uint32_t m[8];  // c · 2^e
-    m[0] = c;
-    for (int e = 1; e < 8; ++e) m[e] = ((m[e - 1] << 1) ^ ((m[e - 1] & 0x80u) ? 0x11Bu : 0u)) & 0xFFu;
-    uint32_t word = 0x10u << 24;
-    for (int b3 = 0; b3 < 3; ++b3) {
-        const int n = 3 * d + b3;
-        uint32_t idx = 0;
-        if (n < 16) {
-            const int o = n >> 1, h = n & 1;
-            for (int b = 0; b < 4; ++b) idx |= ((m[4 * h + b] >> o) & 1u) << b;
-        }
-        word |= (0x10u | idx) << (8 * b3);
-    }
-    stream[((int64_t(obj) * row_tiles + rt) * n_in + j) * (kBsRows * kBsRowDwords) + threadIdx.x] = word;
-}
-
-__global__ __launch_bounds__(kThreads) void gf_matmul_bs_kernel(MatmulParams p, const uint32_t *stream,
-                                                                int row_tiles, int col_blocks) {
-    int rt, cb, obj;
-    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
-    const int row0 = rt * kBsRows;
-    const int rows = min(kBsRows, p.n_out - row0);
-    if (p.hdr != nullptr && cb == 0) {
-        Tile t;
-        t.obj = obj;
-        t.cb = 0;
-        t.row0 = row0;
-        t.rows_here = rows;
-        copy_header(p, t);
-    }
-    const uint8_t *src = p.in + int64_t(obj) * p.in_obj + int64_t(cb) * kBsColBlock;
-    uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0) * p.out_row + int64_t(cb) * kBsColBlock;
-    const uint32_t *idx = stream + (int64_t(obj) * row_tiles + rt) * p.n_in * (kBsRows * kBsRowDwords);
-    const uint32_t off = (threadIdx.x >> 6) * 4096u + (threadIdx.x & 63u) * 16u;
-    // M0 is clobbered on purpose (it carries the XOR index); nothing else in this kernel uses it
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-    asm volatile(RLNC_BS_ASM
-                 :
-                 : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),
-                   [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows), [off] "v"(off)
-                 : RLNC_BS_CLOBBER_V, RLNC_BS_CLOBBER_S);
-#pragma clang diagnostic pop
-}
-
-// Full 16 KiB column blocks of aligned operands; the caller sends the rest elsewhere.
-bool bs_eligible(const MatmulParams &p, bool aligned) {
-    return aligned && p.width >= kBsColBlock && p.n_out >= 4 && p.in_row < (int64_t(1) << 32) &&
-           p.out_row < (int64_t(1) << 32);
-}
-
-size_t bs_scratch_bytes(const MatmulParams &p) {
-    const int64_t tiles = (p.n_out + kBsRows - 1) / kBsRows;
-    // + one step: the main loop prefetches one index step past the end of the last tile
-    return size_t(int64_t(p.n_obj) * tiles * p.n_in * kBsRows * kBsRowDwords * 4 + 256);
-}
-
-hipError_t launch_bs(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full) {
-    full = (p.width / kBsColBlock) * kBsColBlock;
-    const int row_tiles = (p.n_out + kBsRows - 1) / kBsRows;
-    const int col_blocks = int(full / kBsColBlock);
-    const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
-    if (scratch == nullptr || scratch_bytes < bs_scratch_bytes(p)) return hipErrorInvalidValue;
-    if (total > 0x7FFFFFFFLL || p.n_in > 65535 || row_tiles > 65535 || p.n_obj > 65535) return hipErrorInvalidValue;
-    uint32_t *stream = static_cast<uint32_t *>(scratch);
-    hipLaunchKernelGGL(bs_index_kernel, dim3(unsigned(p.n_in), unsigned(row_tiles), unsigned(p.n_obj)),
-                       dim3(64), 0, s, p.coef, p.coef_obj, p.coef_row, p.n_out, p.n_in, row_tiles,
-                       stream);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    MatmulParams q = p;
-    q.width = full;
-    hipLaunchKernelGGL(gf_matmul_bs_kernel, dim3(unsigned(total)), dim3(kThreads), 0, s, q, stream, row_tiles,
-                       col_blocks);
-    return hipGetLastError();
-}
-
-#endif  // RLNC_AB_VARIANTS
 
 // ---------------------------------------------------------------------------------------------------
 // Bit-sliced variant with one code block per coefficient (gen_bsjump.py has the derivation): the (row,
 // source) work is a call into block c -- 16 v_bitop3_b32 XOR3s with the combination registers baked in and
 // only the accumulator relative to the row slot -- instead of 32 GPR-index-relative XORs + 16 M0 writes.
 // ---------------------------------------------------------------------------------------------------
-#ifdef RLNC_BSJ_ASM_FILE  // diagnostic builds substitute a generated variant
-#include RLNC_BSJ_ASM_FILE
-#else
-#ifdef RLNC_BSJ_INC  // A/B builds of the generated program (scripts/bsj_layout_ab.sh)
-#include RLNC_BSJ_INC
-#else
-#include "bitslice_jump.inc"
-#endif
-#endif
-
-constexpr int kBsjWaveRows = RLNC_BSJ_NT;  // output rows per wave; a workgroup of W waves = 8 W rows
-constexpr int kBsjColBlock = 4096;          // 64 lanes × 64 B, shared by the W waves
-
-#ifdef RLNC_BSJ_SOFFSETS  // the shared programs' blocks packed at their own sizes (gen_bsjump.py --pack)
+// The program, its constants and the tile body: bsj_tile.hpp.  The shared programs' blocks are packed at their own
+// sizes (gen_bsjump.py), at these offsets from the table base:
 __constant__ uint32_t kBsjSharedOff[256] = RLNC_BSJ_SOFFSETS;
-#endif
 
 // stream[obj][row tile][j][row in tile] = c · RLNC_BSJ_BLOCK_BYTES (c = 0 for rows past n_out); ABS: the
-// block's absolute address (64-bit, the shared-set programs call it directly): base + kBsjSharedOff[c] for their
-// packed table, base + c · RLNC_BSJ_BLOCK_BYTES for a fixed-stride one (gen_bsjump.py --no-pack)
+// block's absolute address (64-bit, the shared-set programs call it directly): base + kBsjSharedOff[c]
 template <bool ABS>
 __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, int64_t coef_obj, int64_t coef_row,
                                                          int n_out, int n_in, int row_tiles, int tile_rows,
@@ -1108,127 +553,25 @@ __global__ __launch_bounds__(256) void bsj_offset_kernel(const uint8_t *coef, in
     const int row = rt * tile_rows + i;
     const uint32_t c = row < n_out ? coef[int64_t(obj) * coef_obj + int64_t(row) * coef_row + j] : 0u;
     if constexpr (ABS)
-#ifdef RLNC_BSJ_SOFFSETS
         static_cast<uint64_t *>(stream)[int64_t(obj) * per_obj + e] = base + kBsjSharedOff[c];
-#else
-        static_cast<uint64_t *>(stream)[int64_t(obj) * per_obj + e] = base + uint64_t(c) * RLNC_BSJ_BLOCK_BYTES;
-#endif
     else
         static_cast<uint32_t *>(stream)[int64_t(obj) * per_obj + e] = c * uint32_t(RLNC_BSJ_BLOCK_BYTES);
 }
 
-// SHARE (W = 4 only): wave w builds one of the four combination sets of each source row and the sets are
-// exchanged through LDS (RLNC_BSJ_ASM_W4S) instead of every wave building all four
-// probe != nullptr (SHARE only): store the block table's address there and return (launch_bsj, once per device)
-// RUN (W = 8 only, variant 9): the workgroup walks `run` consecutive column blocks of one (object, row tile) --
-// the column-run program (RLNC_BSJ_ASM_W8R) carries the source-row stream across the tile boundaries, so only the
-// first tile pays the prologue (first DMAs, first sets); the grid is objects x row tiles x runs
-// The tile of one workgroup: output rows [rt * 8W, +8W) x column block cb of object obj (the uniform batch
-// kernel below and the ragged kernel both end here).
-template <int W, bool SHARE, bool RUN>
-__device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stream, int row_tiles, int rt, int cb,
-                                         int obj, uint32_t tiles, uint64_t *probe) {
-    constexpr int kTileRows = kBsjWaveRows * W;
-    // W = 8: one workgroup per CU, so a deeper ring and 2 BAR8 set slots (the builders run BAR8 rows ahead)
-    __shared__ __attribute__((aligned(16))) uint8_t ring[(W == 8 ? RLNC_BSJ_SLOTS8 : RLNC_BSJ_SLOTS) * kBsjColBlock];
-    __shared__ __attribute__((aligned(16))) uint8_t cset[SHARE ? (W == 8 ? RLNC_BSJ_CSET_BYTES8 : RLNC_BSJ_CSET_BYTES) : 16];
-    const int row0 = rt * kTileRows;
-    const int rows = min(kTileRows, p.n_out - row0);
-    if (p.hdr != nullptr && cb == 0) {  // coded-piece header (encoder.rs:246-248), 64·W threads
-        const uint8_t *coef_base = p.coef + int64_t(obj) * p.coef_obj + int64_t(row0) * p.coef_row;
-        uint8_t *h = p.hdr + int64_t(obj) * p.hdr_obj + int64_t(row0) * p.hdr_row;
-        for (int e = threadIdx.x; e < rows * p.n_in; e += 64 * W) {
-            const int i = e / p.n_in, j = e % p.n_in;
-            h[int64_t(i) * p.hdr_row + j] = coef_base[int64_t(i) * p.coef_row + j];
-        }
-    }
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lane = threadIdx.x & 63u;
-    const int rows_w = __builtin_amdgcn_readfirstlane(max(0, min(kBsjWaveRows, rows - kBsjWaveRows * w)));
-    const uint8_t *src = p.in + int64_t(obj) * p.in_obj + int64_t(cb) * kBsjColBlock;
-    uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0 + kBsjWaveRows * w) * p.out_row +
-                   int64_t(cb) * kBsjColBlock;
-    constexpr int kEntry = SHARE ? 8 : 4;  // bytes per stream entry: absolute address / block offset
-    const uint8_t *idx = static_cast<const uint8_t *>(stream) +
-                         ((int64_t(obj) * row_tiles + rt) * p.n_in * kTileRows + kBsjWaveRows * w) * kEntry;
-    typedef __attribute__((address_space(3))) uint8_t lds_u8;
-    const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)ring));  // addrspacecast
-    // W = 8 (shared): waves 0-3 stage the ring and build the sets exactly as in the 4-wave program, waves 4-7
-    // (cons = 1) only read the sets and call
-    constexpr int kStageWaves = (SHARE && W == 8) ? 4 : W;
-    const int ws = w % kStageWaves;
-    constexpr uint32_t kShare = kBsjColBlock / kStageWaves;  // bytes of each row a wave moves into the ring
-    const uint32_t ldsw = __builtin_amdgcn_readfirstlane(ring_lds + kShare * uint32_t(ws));
-    const uint32_t ldsr = ring_lds + 16u * lane;
-    const uint32_t dmaoff = kShare * uint32_t(ws) + 16u * lane;
-    const uint32_t off = 16u * lane;
-    const uint32_t ldsc = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)cset)) + 16u * lane;
-    const uint32_t ldscw = ldsc + 4096u * uint32_t(ws);      // this wave's set (group ws >> 1, half ws & 1)
-    const uint32_t ldsrg = ldsr + 2048u * uint32_t(ws >> 1);  // this wave's group of the ring chunk
-    const uint32_t half = uint32_t(ws & 1);
-    const uint32_t cons = uint32_t(w / kStageWaves);
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-#define RLNC_BSJ_OPERANDS                                                                                            \
-    : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),                           \
-      [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw), [off] "v"(off), \
-      [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr), [ldsc] "v"(ldsc), [ldscw] "v"(ldscw), [ldsrg] "v"(ldsrg),           \
-      [half] "s"(half), [probe] "s"(probe), [cons] "s"(cons), [ldsc2] "v"(ldsc + 65536u),                        \
-      [ldscw2] "v"(ldscw + 65536u), [tiles] "s"(tiles)                                                            \
-    : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S
-    if constexpr (W == 1) asm volatile(RLNC_BSJ_ASM_W1 : RLNC_BSJ_OPERANDS);
-    if constexpr (W == 2) asm volatile(RLNC_BSJ_ASM_W2 : RLNC_BSJ_OPERANDS);
-    if constexpr (W == 4 && !SHARE) asm volatile(RLNC_BSJ_ASM_W4 : RLNC_BSJ_OPERANDS);
-    if constexpr (W == 4 && SHARE) asm volatile(RLNC_BSJ_ASM_W4S : RLNC_BSJ_OPERANDS);
-    if constexpr (W == 8 && !RUN) asm volatile(RLNC_BSJ_ASM_W8S : RLNC_BSJ_OPERANDS);
-    if constexpr (W == 8 && RUN) asm volatile(RLNC_BSJ_ASM_W8R : RLNC_BSJ_OPERANDS);
-#undef RLNC_BSJ_OPERANDS
-#pragma clang diagnostic pop
+
+
+template <int W, bool SHARE = false>
+__global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const void *stream, int row_tiles,
+                                                               int col_blocks, uint64_t *probe) {
+    static_assert(!SHARE || W == 4 || W == 8, "the shared-set programs are generated for 4 and 8 waves");
+    int rt, cb, obj;
+    decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
+    bsj_tile<W, SHARE, false>(p, stream, row_tiles, rt, cb, obj, 1u, nullptr);
 }
 
-
-template <int W, bool SHARE = false, bool RUN = false>
-__global__ __launch_bounds__(64 * W) void gf_matmul_bsj_kernel(MatmulParams p, const void *stream, int row_tiles,
-                                                               int col_blocks, uint64_t *probe, int run = 1,
-                                                               int guided_nl = -1) {
-    static_assert(!SHARE || W == 4 || W == 8, "the shared-set programs are generated for 4 and 8 waves");
-    // (a 4-wave run program measured no gain: two workgroups per CU already hide the 32-row tile's prologue,
-    // profiles/r02_run_ab.txt)
-    static_assert(!RUN || (W == 8 && SHARE), "the column-run program is generated for the 8-wave shared program");
-    int rt, cb, obj;
-    uint32_t tiles = 1;
-    if constexpr (RUN) {
-        const int runs = (col_blocks + run - 1) / run;
-        int r;
-        if (guided_nl < 0) {
-            decode_block(p.n_obj * row_tiles * runs, row_tiles, runs, rt, r, obj);
-            cb = r * run;
-            tiles = uint32_t(__builtin_amdgcn_readfirstlane(min(run, col_blocks - cb)));
-        } else {
-            // guided runs (launch_bsj checked: run | col_blocks, 8 | the run units): XCD x = b & 7 owns run units
-            // [x·per, (x+1)·per) (rt fastest, as decode_block), its first guided_nl dispatched workgroups walk one
-            // unit each, the later ones one column block of the remaining units -- short workgroups last
-            const int per = (p.n_obj * row_tiles * runs) >> 3;
-            const int b = blockIdx.x, x = b & 7, i = b >> 3;
-            int u, c = 0;
-            if (i < guided_nl) {
-                u = x * per + i;
-                tiles = uint32_t(run);
-            } else {
-                const int j = i - guided_nl;
-                u = x * per + guided_nl + j / run;
-                c = j % run;
-            }
-            rt = u % row_tiles;
-            const int rest = u / row_tiles;
-            r = rest % runs;
-            obj = rest / runs;
-            cb = r * run + c;
-        }
-    } else {
-        decode_block(p.n_obj * row_tiles * col_blocks, row_tiles, col_blocks, rt, cb, obj);
-    }
-    bsj_tile<W, SHARE, RUN>(p, stream, row_tiles, rt, cb, obj, tiles, probe);
+// the shared program's probe launch: stores its block table's address and returns (bsj_shared_base)
+__global__ __launch_bounds__(256) void gf_matmul_bsj_probe_kernel(MatmulParams p, const void *stream, uint64_t *probe) {
+    bsj_tile<4, true, false>(p, stream, 1, 0, 0, 0, 1u, probe);
 }
 
 // waves per workgroup: 8 output rows each, at most 4 (a 32-row tile), no more than the rows need
@@ -1271,7 +614,7 @@ static hipError_t bsj_shared_base(hipStream_t s, void *scratch, uint64_t &base) 
         q.n_out = 1;
         q.n_in = 1;
         uint64_t *slot = static_cast<uint64_t *>(scratch);
-        hipLaunchKernelGGL((gf_matmul_bsj_kernel<4, true>), dim3(1), dim3(256), 0, s, q, scratch, 1, 1, slot);
+        hipLaunchKernelGGL(gf_matmul_bsj_probe_kernel, dim3(1), dim3(256), 0, s, q, scratch, slot);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         uint64_t h = 0;
         if ((e = hipMemcpyAsync(&h, slot, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
@@ -1283,44 +626,13 @@ static hipError_t bsj_shared_base(hipStream_t s, void *scratch, uint64_t &base) 
     return hipSuccess;
 }
 
-#ifdef RLNC_AB_VARIANTS  // variant 9 (column runs): A/B history, diagnostic builds only
-// Column blocks per workgroup of the column-run program: enough runs for >= 4 workgroups per CU, at most 8
-// blocks each (RLNC_BSJ_RUN = n forces n; A/B knob, read once)
-static int bsj_run_length(int64_t tiles, int col_blocks, int requested) {
-    static const int forced = [] {
-        const char *e = getenv("RLNC_BSJ_RUN");
-        return e ? atoi(e) : 0;
-    }();
-    static std::mutex mu;
-    static int cus[64] = {};
-    int dev = 0, n = 256;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-        std::lock_guard<std::mutex> lock(mu);
-        if (cus[dev] == 0 && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus[dev] = 256;
-        n = cus[dev] > 0 ? cus[dev] : 256;
-    }
-    int r = requested > 0 ? requested
-            : forced > 0  ? forced
-                          : int(std::min<int64_t>(8, std::max<int64_t>(1, tiles / (int64_t(n) * 4))));
-    return std::max(1, std::min(r, col_blocks));
-}
+}  // namespace
 
-// Guided column runs (variant 9): percentage of each XCD's run units walked as whole runs, the rest as single
-// column blocks dispatched last (RLNC_BSJ_GUIDED; -1 = plain runs).  A/B knob, read once.
-static int bsj_guided_pct() {
-    static const int pct = [] {
-        const char *e = getenv("RLNC_BSJ_GUIDED");
-        return e ? std::max(-1, std::min(100, atoi(e))) : -1;
-    }();
-    return pct;
-}
-
-#endif  // RLNC_AB_VARIANTS
-
-hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full,
-                      bool share, bool wide, bool run) {
-    full = (p.width / kBsjColBlock) * kBsjColBlock;
+// The block-address stream of a bit-sliced jump product (one bsj_offset_kernel launch) and the launch geometry of its
+// whole 4 KiB column blocks (kernels.hpp BsjPlan)
+hipError_t bsj_prepare(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, bool share,
+                       bool wide, BsjPlan &b) {
+    b.full = (p.width / kBsjColBlock) * kBsjColBlock;
     if (scratch == nullptr || scratch_bytes < bsj_scratch_bytes(p, share && wide)) return hipErrorInvalidValue;
     int W = bsj_waves(p.n_out, share && wide);
     bool abs = share && W >= 4;  // the shared-set programs call absolute block addresses
@@ -1333,57 +645,51 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
         if (!abs) W = bsj_waves(p.n_out);
     }
     const int tile_rows = kBsjWaveRows * W;
-    const int row_tiles = (p.n_out + tile_rows - 1) / tile_rows;
-    const int col_blocks = int(full / kBsjColBlock);
-    const int64_t total = int64_t(p.n_obj) * row_tiles * col_blocks;
-    if (total > 0x7FFFFFFFLL || p.n_obj > 65535) return hipErrorInvalidValue;
-    void *stream = scratch;
-    const int64_t per_obj = int64_t(row_tiles) * p.n_in * tile_rows;
+    b.waves = W;
+    b.share = share;
+    b.row_tiles = (p.n_out + tile_rows - 1) / tile_rows;
+    b.col_blocks = int(b.full / kBsjColBlock);
+    b.total = int64_t(p.n_obj) * b.row_tiles * b.col_blocks;
+    if (b.total > 0x7FFFFFFFLL || p.n_obj > 65535) return hipErrorInvalidValue;
+    b.stream = scratch;
+    const int64_t per_obj = int64_t(b.row_tiles) * p.n_in * tile_rows;
     if ((per_obj + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
     const dim3 og(unsigned((per_obj + 255) / 256), unsigned(p.n_obj));
     if (abs)
         hipLaunchKernelGGL(bsj_offset_kernel<true>, og, dim3(256), 0, s, p.coef, p.coef_obj, p.coef_row, p.n_out,
-                           p.n_in, row_tiles, tile_rows, stream, base);
+                           p.n_in, b.row_tiles, tile_rows, b.stream, base);
     else
         hipLaunchKernelGGL(bsj_offset_kernel<false>, og, dim3(256), 0, s, p.coef, p.coef_obj, p.coef_row, p.n_out,
-                           p.n_in, row_tiles, tile_rows, stream, uint64_t(0));
-    hipError_t e = hipGetLastError();
+                           p.n_in, b.row_tiles, tile_rows, b.stream, uint64_t(0));
+    return hipGetLastError();
+}
+
+namespace {
+
+hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, int64_t &full,
+                      bool share, bool wide) {
+    BsjPlan b;
+    hipError_t e = bsj_prepare(p, s, scratch, scratch_bytes, share, wide, b);
+    full = b.full;
     if (e != hipSuccess) return e;
     MatmulParams q = p;
-    q.width = full;
-    if (W == 1)
-        hipLaunchKernelGGL(gf_matmul_bsj_kernel<1>, dim3(unsigned(total)), dim3(64), 0, s, q, stream, row_tiles,
-                           col_blocks, nullptr);
-    else if (W == 2)
-        hipLaunchKernelGGL(gf_matmul_bsj_kernel<2>, dim3(unsigned(total)), dim3(128), 0, s, q, stream, row_tiles,
-                           col_blocks, nullptr);
-#ifdef RLNC_AB_VARIANTS
-    else if (W == 8 && run) {
-        const int rl = bsj_run_length(total, col_blocks, p.col_run);
-        const int64_t units = int64_t(p.n_obj) * row_tiles * ((col_blocks + rl - 1) / rl);
-        const int pct = bsj_guided_pct();
-        if (pct >= 0 && rl > 1 && col_blocks % rl == 0 && units % 8 == 0) {
-            // guided: per XCD, pct % of the run units as whole runs (dispatched first), the rest one block each
-            const int64_t per = units / 8;
-            const int64_t nl = per * pct / 100;
-            const int64_t wgs = 8 * (nl + (per - nl) * rl);
-            hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true, true>), dim3(unsigned(wgs)), dim3(512), 0, s, q, stream,
-                               row_tiles, col_blocks, nullptr, rl, int(nl));
-        } else {
-            hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true, true>), dim3(unsigned(units)), dim3(512), 0, s, q,
-                               stream, row_tiles, col_blocks, nullptr, rl, -1);
-        }
-    }
-#endif
-    else if (W == 8)
-        hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true>), dim3(unsigned(total)), dim3(512), 0, s, q, stream,
-                           row_tiles, col_blocks, nullptr);
-    else if (share)
-        hipLaunchKernelGGL((gf_matmul_bsj_kernel<4, true>), dim3(unsigned(total)), dim3(256), 0, s, q, stream,
-                           row_tiles, col_blocks, nullptr);
+    q.width = b.full;
+    const dim3 grid(unsigned(b.total));
+    if (b.waves == 1)
+        hipLaunchKernelGGL(gf_matmul_bsj_kernel<1>, grid, dim3(64), 0, s, q, b.stream, b.row_tiles, b.col_blocks,
+                           nullptr);
+    else if (b.waves == 2)
+        hipLaunchKernelGGL(gf_matmul_bsj_kernel<2>, grid, dim3(128), 0, s, q, b.stream, b.row_tiles, b.col_blocks,
+                           nullptr);
+    else if (b.waves == 8)
+        hipLaunchKernelGGL((gf_matmul_bsj_kernel<8, true>), grid, dim3(512), 0, s, q, b.stream, b.row_tiles,
+                           b.col_blocks, nullptr);
+    else if (b.share)
+        hipLaunchKernelGGL((gf_matmul_bsj_kernel<4, true>), grid, dim3(256), 0, s, q, b.stream, b.row_tiles,
+                           b.col_blocks, nullptr);
     else
-        hipLaunchKernelGGL(gf_matmul_bsj_kernel<4>, dim3(unsigned(total)), dim3(256), 0, s, q, stream, row_tiles,
-                           col_blocks, nullptr);
+        hipLaunchKernelGGL(gf_matmul_bsj_kernel<4>, grid, dim3(256), 0, s, q, b.stream, b.row_tiles, b.col_blocks,
+                           nullptr);
     return hipGetLastError();
 }
 
@@ -1453,11 +759,7 @@ __global__ __launch_bounds__(256) void ragged_offset_kernel(const RaggedObj *obj
     const int rt = int(l / (int64_t(tr) * d.n_in));
     const int row = rt * tr + i;
     const uint32_t c = row < d.n_out ? d.coef[int64_t(row) * d.coef_row + j] : 0u;
-#ifdef RLNC_BSJ_SOFFSETS
     stream[e] = base + kBsjSharedOff[c];
-#else
-    stream[e] = base + uint64_t(c) * RLNC_BSJ_BLOCK_BYTES;
-#endif
 }
 
 template <int W>
@@ -1855,7 +1157,12 @@ static hipError_t launch_realign(uint8_t *dst, int64_t dst_row, int64_t dst_obj,
 
 static bool jump_variant(MatmulVariant v) {
     return v == MatmulVariant::BitSlicedJump || v == MatmulVariant::BitSlicedJumpShared ||
-           v == MatmulVariant::BitSlicedJumpShared8 || v == MatmulVariant::BitSlicedJumpRun;
+           v == MatmulVariant::BitSlicedJumpShared8;
+}
+
+// the shipped variants; the others (2-5, 9) are the A/B history of kernels_ab.hip (make ab)
+static bool shipped_variant(MatmulVariant v) {
+    return v == MatmulVariant::Perm || v == MatmulVariant::NibbleLds || jump_variant(v);
 }
 
 struct RealignPlan {
@@ -1899,30 +1206,22 @@ static bool realign_plan(const MatmulParams &p, MatmulVariant v, RealignPlan &r)
 }
 
 size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v) {
+    if (!shipped_variant(v)) return matmul_scratch_bytes_ab(p, v);
     RealignPlan r;
     if (realign_plan(p, v, r)) return r.prod_bytes + r.in_bytes + r.out_bytes;
     return matmul_scratch_bytes_aligned(p, v);
 }
 
 size_t matmul_scratch_bytes_aligned(const MatmulParams &p, MatmulVariant v) {
-    if ((v != MatmulVariant::BitSliced && v != MatmulVariant::BitSlicedJump && v != MatmulVariant::BitSlicedJumpShared &&
-         v != MatmulVariant::BitSlicedJumpShared8 && v != MatmulVariant::BitSlicedJumpRun) ||
-        p.n_out <= 0 || p.n_in <= 0 || p.n_obj <= 0)
-        return 0;
-#ifdef RLNC_AB_VARIANTS
-    if (v == MatmulVariant::BitSliced) return bs_eligible(p, matmul_aligned(p)) ? bs_scratch_bytes(p) : 0;
-#else
-    if (v == MatmulVariant::BitSliced) return 0;
-#endif
-    return bsj_eligible(p, matmul_aligned(p))
-               ? bsj_scratch_bytes(p, v == MatmulVariant::BitSlicedJumpShared8 || v == MatmulVariant::BitSlicedJumpRun)
-               : 0;
+    if (!jump_variant(v) || p.n_out <= 0 || p.n_in <= 0 || p.n_obj <= 0) return 0;
+    return bsj_eligible(p, matmul_aligned(p)) ? bsj_scratch_bytes(p, v == MatmulVariant::BitSlicedJumpShared8) : 0;
 }
 
 hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, void *scratch, size_t scratch_bytes) {
     if (p.n_out <= 0 || p.width <= 0 || p.n_obj <= 0) return hipSuccess;
     const bool aligned = matmul_aligned(p);
     if (p.n_in <= 0) return hipErrorInvalidValue;
+    if (!shipped_variant(v)) return launch_matmul_ab(p, s, v, scratch, scratch_bytes);
     RealignPlan r;
     if (realign_plan(p, v, r)) {  // misaligned rows: realign copies around the aligned product
         if (scratch == nullptr || scratch_bytes < r.prod_bytes + r.in_bytes + r.out_bytes) return hipErrorInvalidValue;
@@ -1962,8 +1261,7 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
         }
         return hipSuccess;
     }
-    const bool jump = v == MatmulVariant::BitSlicedJump || v == MatmulVariant::BitSlicedJumpShared ||
-                      v == MatmulVariant::BitSlicedJumpShared8 || v == MatmulVariant::BitSlicedJumpRun;
+    const bool jump = jump_variant(v);
     if (jump && aligned && p.n_out <= 3 && p.width >= kColBlock) {
         // one to three coded pieces per source pass: HBM-bound, streamed with deep prefetch
         const int64_t full = (p.width / kColBlock) * kColBlock;
@@ -1979,28 +1277,13 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
         t.hdr = nullptr;
         return launch_matmul(t, s, MatmulVariant::Perm);
     }
-#ifndef RLNC_AB_VARIANTS
-    if (v != MatmulVariant::Perm && v != MatmulVariant::NibbleLds && v != MatmulVariant::BitSlicedJump &&
-        v != MatmulVariant::BitSlicedJumpShared && v != MatmulVariant::BitSlicedJumpShared8)
-        return hipErrorInvalidValue;  // the A/B variants exist in diagnostic builds only
-#endif
-    if (v == MatmulVariant::BitSliced || jump) {
-        const bool run = v == MatmulVariant::BitSlicedJumpRun;
-        const bool share = v == MatmulVariant::BitSlicedJumpShared || v == MatmulVariant::BitSlicedJumpShared8 || run;
-        const bool wide = v == MatmulVariant::BitSlicedJumpShared8 || run;
+    if (jump) {
+        const bool share = v == MatmulVariant::BitSlicedJumpShared || v == MatmulVariant::BitSlicedJumpShared8;
+        const bool wide = v == MatmulVariant::BitSlicedJumpShared8;
         v = MatmulVariant::Perm;  // whatever the bit-sliced kernels do not cover
-#ifdef RLNC_AB_VARIANTS
-        if (jump ? bsj_eligible(p, aligned) : bs_eligible(p, aligned)) {
-#else
         if (bsj_eligible(p, aligned)) {
-#endif
             int64_t full = 0;
-#ifdef RLNC_AB_VARIANTS
-            hipError_t e = jump ? launch_bsj(p, s, scratch, scratch_bytes, full, share, wide, run)
-                                : launch_bs(p, s, scratch, scratch_bytes, full);
-#else
-            hipError_t e = launch_bsj(p, s, scratch, scratch_bytes, full, share, wide, run);
-#endif
+            hipError_t e = launch_bsj(p, s, scratch, scratch_bytes, full, share, wide);
             if (e != hipSuccess || full == p.width) return e;
             MatmulParams t = p;
             t.in = p.in + full;
@@ -2010,15 +1293,6 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
             return launch_matmul(t, s, v);
         }
     }
-#ifdef RLNC_AB_VARIANTS
-    if (aligned && (v == MatmulVariant::Wide || v == MatmulVariant::Wide4)) {
-        if (v == MatmulVariant::Wide4) return p.n_out <= 4 ? launch_wide_split<4, 4>(p, s) : launch_wide_split<8, 4>(p, s);
-        if (p.n_out <= 4) return launch_wide_split<4, 2>(p, s);
-        if (p.n_out <= 8) return launch_wide_split<8, 2>(p, s);
-        return launch_wide_split<16, 2>(p, s);
-    }
-    if (v == MatmulVariant::Wide || v == MatmulVariant::Wide4) v = MatmulVariant::Perm;
-#endif
     // narrow (< one 4 KiB column block, e.g. the ragged tail of a recode over k + L bytes): the work is the
     // sources x rows chain of one block, so split the rows over many workgroups (2 rows each)
     // (1-2 rows too while the sources are few, e.g. the short tail of one recoded piece: 107 -> 80 us per
@@ -2036,6 +1310,16 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
     if (p.n_out <= 16) return launch_nt<16>(p, s, v, aligned);
     return launch_nt<32>(p, s, v, aligned);
 }
+
+bool bsj_eligible_public(const MatmulParams &p) { return bsj_eligible(p, matmul_aligned(p)); }
+size_t bsj_scratch_bytes_public(const MatmulParams &p, bool wide) { return bsj_scratch_bytes(p, wide); }
+
+// The A/B build (make ab) links kernels_ab.hip, whose definitions replace these
+__attribute__((weak)) bool ab_build() { return false; }
+__attribute__((weak)) hipError_t launch_matmul_ab(const MatmulParams &, hipStream_t, MatmulVariant, void *, size_t) {
+    return hipErrorInvalidValue;  // the A/B variants exist in the diagnostic build only
+}
+__attribute__((weak)) size_t matmul_scratch_bytes_ab(const MatmulParams &, MatmulVariant) { return 0; }
 
 bool ragged_bsj_eligible(const uint8_t *in, const uint8_t *out, int64_t in_row, int64_t out_row, int64_t width,
                          int n_out) {

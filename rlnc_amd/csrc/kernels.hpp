@@ -57,6 +57,29 @@ bool unaligned_vector_ok();
 hipError_t launch_matmul(const MatmulParams &p, hipStream_t stream, MatmulVariant v = MatmulVariant::Perm,
                          void *scratch = nullptr, size_t scratch_bytes = 0);
 
+struct RrefParams;
+
+// ---- the A/B build (make ab: kernels_ab.hip adds matmul variants 2-5 and 9, rref_ab.hip decode paths 3, 4, 6) ----
+// The shipped library defines these weakly (ab_build() false, the launches hipErrorInvalidValue); the A/B build's
+// definitions replace them.
+bool ab_build();
+bool launch_rref_ab(const RrefParams &p, hipStream_t s, hipError_t *result);  // true: launched (*result its status)
+hipError_t launch_matmul_ab(const MatmulParams &p, hipStream_t s, MatmulVariant v, void *scratch, size_t scratch_bytes);
+size_t matmul_scratch_bytes_ab(const MatmulParams &p, MatmulVariant v);
+// what the A/B variants reuse of the shipped bit-sliced jump path (kernels.hip): eligibility (whole 4 KiB column blocks
+// of aligned operands, >= 4 output rows), scratch size, and the block-address stream + launch geometry of a product
+struct BsjPlan {
+    int64_t full = 0;   // columns the bit-sliced program takes (whole 4 KiB blocks)
+    int64_t total = 0;  // workgroups of the uniform launch
+    int waves = 0, row_tiles = 0, col_blocks = 0;
+    bool share = false;
+    void *stream = nullptr;  // the block-address stream (in the scratch)
+};
+bool bsj_eligible_public(const MatmulParams &p);
+size_t bsj_scratch_bytes_public(const MatmulParams &p, bool wide);
+hipError_t bsj_prepare(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, bool share, bool wide,
+                       BsjPlan &b);
+
 // ---- ragged batches: one launch per kernel stage over objects of different shapes (wire.hip) -----------------
 // One object's part of a ragged matmul launch (device-side descriptor table, 120 bytes).  Objects are ordered by
 // wg0 (and, in the block-address stream, by idx0).

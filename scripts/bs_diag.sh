@@ -11,7 +11,5 @@ for d in ${DIAGS:-novm nosmem novm,nosmem}; do
   out=$ROOT/build/diag_$name
   mkdir -p "$out/obj"
   python3 rlnc_amd/csrc/gen_bitslice.py --diag "$d" --out "$out/bitslice_asm.inc"
-  make -s -C rlnc_amd/csrc OUT="$out/librlnc_hip.so" OBJDIR="$out/obj" \
-       CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -DRLNC_BS_ASM_FILE=\\\"$out/bitslice_asm.inc\\\""
-  echo "built $out/librlnc_hip.so"
+  AB=1 scripts/diag_build.sh "$out" "bitslice_asm.inc=$out/bitslice_asm.inc"  # variant 5 lives in the A/B build
 done

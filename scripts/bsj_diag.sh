@@ -9,7 +9,5 @@ for spec in $DIAGS; do
   out=$ROOT/build/diag_$name
   mkdir -p "$out/obj"
   python3 rlnc_amd/csrc/gen_bsjump.py $args --out "$out/bitslice_jump.inc"
-  make -s -C rlnc_amd/csrc OUT="$out/librlnc_hip.so" OBJDIR="$out/obj" \
-       CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -DRLNC_BSJ_ASM_FILE=\\\"$out/bitslice_jump.inc\\\""
-  echo "built $out/librlnc_hip.so"
+  scripts/diag_build.sh "$out" "bitslice_jump.inc=$out/bitslice_jump.inc"
 done

@@ -9,9 +9,7 @@ build() {  # name load-hint store-hint
   out=$ROOT/build/var/$1
   mkdir -p "$out/obj"
   python3 rlnc_amd/csrc/gen_bsjump.py --out "$out/bitslice_jump.inc" --load-hint "$2" --store-hint "$3"
-  make -s -C rlnc_amd/csrc OUT="$out/librlnc_hip.so" OBJDIR="$out/obj" \
-       CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -DRLNC_BSJ_ASM_FILE=\\\"$out/bitslice_jump.inc\\\""
-  echo "built $out/librlnc_hip.so"
+  scripts/diag_build.sh "$out" "bitslice_jump.inc=$out/bitslice_jump.inc"
 }
 build stnt "" "nt" &
 build ldnt "nt" "" &

@@ -1,7 +1,7 @@
-# the whole -m gpu suite (fail-fast), then the HSA dispatch probe and the piece A/B
+# the whole -m gpu suite on the shipped library (fail-fast), then the A/B build's variant tests
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 1000 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_lifetime.py tests/test_gpu_piece.py tests > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
-tail -3 gpurun_out/gpu_tests.log
-timeout -k 10 60 build/ubench_hsa_dispatch > gpurun_out/hsa.jsonl 2>&1
-bash scripts/r04_piece_ab.sh
+timeout -k 10 1000 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
+RLNC_LIB_PATH=$PWD/rlnc_amd/librlnc_hip_ab.so timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_fullrange.py tests/test_gpu_graph.py > gpurun_out/ab_tests.log 2>&1 || { tail -40 gpurun_out/ab_tests.log; exit 1; }
+tail -2 gpurun_out/ab_tests.log
