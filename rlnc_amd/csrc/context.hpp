@@ -207,8 +207,13 @@ struct rlnc_context {
     std::vector<std::unique_ptr<HsSlot>> hs_slots;
     hipStream_t hs_h2d = nullptr, hs_d2h = nullptr;
     DevBuf ws_tab;  // descriptor tables of the wire-format / ragged calls (wire.hip), uploaded from pin_tab
-    PinBuf pin_tab;
-    hipEvent_t tab_ev = nullptr;  // the last descriptor upload (pin_tab may be rewritten once it has run)
+    // a ring of pinned staging buffers, each with the event of its last upload (it may be rewritten once that has
+    // run): a ragged decode stages three tables per call, and with one buffer its third upload waited on the host for
+    // the second's copy, queued behind the whole elimination
+    static constexpr int kTabRing = 4;
+    PinBuf pin_tab[kTabRing];
+    hipEvent_t tab_ev[kTabRing] = {};
+    int tab_next = 0;
     // descriptor tables of calls captured into HIP graphs: bump-allocated, never reused or moved (a replay rewrites
     // exactly its captured bytes); reserved by eager calls, since nothing may be allocated inside a capture
     std::vector<std::unique_ptr<DevBuf>> cap_arenas;
@@ -241,7 +246,8 @@ struct rlnc_context {
             (void)hipStreamDestroy(up_stream);
         }
         for (auto &b : blk) (void)hipFree(b.second);
-        if (tab_ev) (void)hipEventDestroy(tab_ev);
+        for (hipEvent_t e : tab_ev)
+            if (e) (void)hipEventDestroy(e);
         if (own) (void)hipStreamDestroy(own);
         delete this;  // the buffers' destructors free on this device
     }

@@ -776,7 +776,42 @@ def epilogue(L):
     L.append("2:")
 
 
-def program():
+def body_deep(L, j, slots):
+    """body() with a deeper ring (the 1-wave program): `slots` ring slots, source rows j + 1 .. j + slots - 2 in
+    flight while row j is used and row j + slots - 1 issued here; block-offset buffers alternate (j % 2)."""
+    D = slots - 1
+    slot = j % slots
+    L.append(f"s_waitcnt vmcnt({(D - 1) * (4 // WAVES)})")  # this wave's DMAs of row j done
+    if WAVES > 1:
+        L.append("s_barrier")
+    L.append(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
+    advance_s(L)
+    dma(L, (j + D) % slots)  # row j + D into the slot row j - 1 used (read, and waited for, in body j - 1)
+    for g in range(2):
+        for h in range(2):
+            q = 2 * g + h
+            L.append(f"ds_read_b128 v[{RAW(g, 4 * h)}:{RAW(g, 4 * h) + 3}], %[ldsr] offset:{slot * 4096 + q * 1024}")
+    L.append("s_waitcnt lgkmcnt(0)")
+    for g in range(2):
+        planes = {b: G(g, b // 4, 1 << (b % 4)) for b in range(8)}
+        transpose({d: RAW(g, d) for d in range(8)}, planes, L)
+    for g in range(2):
+        for h in range(2):
+            combos(g, h, L)
+    cur, nxt = S_OFF[j % 2], S_OFF[(j + 1) % 2]
+    L += [
+        f"s_load_dwordx8 s[{nxt}:{nxt + 7}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
+        f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
+        f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
+        "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)",
+    ]
+    for i in range(NT):
+        call(L, cur, i)
+    L.append("s_set_gpr_idx_off")
+
+
+def program(slots=SLOTS):
+    """slots > 3: the deeper-ring form (body_deep); slots = 3: rows j + 1, j + 2 in flight (body)."""
     L = [
         f"s_mov_b64 s[{S_SRC}:{S_SRC + 1}], %[src]",
         f"s_mov_b64 s[{S_IDX}:{S_IDX + 1}], %[idx]",
@@ -794,6 +829,25 @@ def program():
         f"s_addc_u32 s{S_BASE + 1}, s{S_BASE + 1}, 0",
         f"s_mov_b32 s{S_LDSW}, %[ldsw]",
     ]
+    if slots > 3:  # rows 0 .. slots - 2 on their way (the last row again past n_in), row 0's offsets
+        L.append(f"s_sub_u32 s{S_NDMA}, %[n_in], 1")
+        for r in range(slots - 1):
+            if r:
+                advance_s(L)
+            dma(L, r)
+        L.append(f"s_load_dwordx8 s[{S_OFF[0]}:{S_OFF[0] + 7}], s[{S_IDX}:{S_IDX + 1}], 0")
+        L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
+        L += [f"v_mov_b32 {v(G(g, h, 0))}, 0" for g in range(2) for h in range(2)]
+        unroll = slots if slots % 2 == 0 else 2 * slots
+        loops(L, lambda LL, j: body_deep(LL, j, slots), unroll)
+        epilogue(L)
+        L.append("s_branch 8f")
+        if ALIGN:
+            L.append(f".p2align {ALIGN}")
+        L.append("9:")
+        blocks(L)
+        L.append("8:")
+        return L
     # prologue: rows 0 and 1 on their way into slots 0 and 1 (row 0 again when n_in == 1), row 0's offsets
     dma(L, 0)
     advance(L)
@@ -847,6 +901,10 @@ def main():
                     help="shared programs: fixed-stride XOR3-only blocks (A/B history: bsj_tile.hpp requires packed)")
     ap.add_argument("--prio", default="", help="K,L: shared program's calls K.. of each row at s_setprio L")
     ap.add_argument("--load-hint", default="", help="cache-policy modifiers of the DMA loads, e.g. 'nt' (A/B)")
+    # 5 slots (4 rows in flight) measured equal to 3 on the 8-row ragged recode of scripts/ragged_rate.py
+    # (0.2228 / 0.2205 ms against 0.2188 / 0.2233, profiles/r04_ragged_ab.txt): the 1-wave program is not waiting on
+    # its source rows there
+    ap.add_argument("--slots1", type=int, default=3, help="ring slots of the 1-wave program (3 = the 2-row form)")
     ap.add_argument("--store-hint", default="", help="cache-policy modifiers of the tile stores, e.g. 'nt' (A/B)")
     args = ap.parse_args()
     HINTS["load"], HINTS["store"] = args.load_hint, args.store_hint
@@ -871,10 +929,11 @@ def main():
         f.write(f"#define RLNC_BSJ_NT {NT}\n")
         f.write(f"#define RLNC_BSJ_SLOTS {SLOTS}\n")
         f.write(f"#define RLNC_BSJ_BLOCK_BYTES {BLOCK_BYTES}\n")
+        f.write(f"#define RLNC_BSJ_SLOTS1 {args.slots1}\n")
         for w in (1, 2, 4):
             WAVES, WG_ROWS = w, NT * w
             STREAM_J_BYTES = WG_ROWS * 4
-            body_txt = "\\n\\t".join(hinted(program()))
+            body_txt = "\\n\\t".join(hinted(program(args.slots1 if w == 1 else SLOTS)))
             f.write(f'#define RLNC_BSJ_ASM_W{w} "{body_txt}"\n')
         WAVES, WG_ROWS = 4, NT * 4
         STREAM_J_BYTES = WG_ROWS * 8  # 64-bit block addresses

@@ -737,8 +737,9 @@ __device__ __forceinline__ MatmulParams ragged_params(const RaggedObj &d) {
 }
 
 // the block-address stream of every object of the table (all wave classes at once): entry e of object o is the
-// absolute address of the code block of coefficient c = coef[row][j] (0 past n_out), laid out [rt][j][row in tile]
-// from objs[o].idx0, as bsj_offset_kernel lays out one object
+// code block of coefficient c = coef[row][j] (0 past n_out), laid out [rt][j][row in tile] from objs[o].idx0 (in
+// 8-byte units), as bsj_offset_kernel lays out one object -- its absolute address for the 4- and 8-wave classes, its
+// 4-byte offset for the 1- and 2-wave ones (whose half-used space the table still reserves at 8 bytes an entry)
 __global__ __launch_bounds__(256) void ragged_offset_kernel(const RaggedObj *objs, int n, int64_t entries,
                                                             uint64_t *stream, uint64_t base) {
     const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
@@ -759,19 +760,26 @@ __global__ __launch_bounds__(256) void ragged_offset_kernel(const RaggedObj *obj
     const int rt = int(l / (int64_t(tr) * d.n_in));
     const int row = rt * tr + i;
     const uint32_t c = row < d.n_out ? d.coef[int64_t(row) * d.coef_row + j] : 0u;
-    stream[e] = base + kBsjSharedOff[c];
+    if (tr > 16)  // the shared-set programs (4 and 8 waves): absolute block addresses
+        stream[e] = base + kBsjSharedOff[c];
+    else  // 1 and 2 waves: block offsets, 4 bytes each, packed from the object's first entry
+        reinterpret_cast<uint32_t *>(stream + d.idx0)[l] = c * uint32_t(RLNC_BSJ_BLOCK_BYTES);
 }
 
 template <int W>
 __global__ __launch_bounds__(64 * W) void gf_matmul_bsj_ragged_kernel(const RaggedObj *objs, int n, int64_t total,
                                                                       const uint64_t *stream) {
-    const int64_t w = xcd_work_index(total);
+    // 1 and 2 waves: objects of <= 16 rows have one row tile, so no two workgroups share source rows (nothing for an
+    // XCD's L2 to keep); the table lists them by source count, most first, and the launch order spreads them over the
+    // XCDs and CUs as they come -- the long tiles start first and side by side, not wherever an XCD's contiguous range
+    // of the launch happens to hold them (8-row recodes of 16-130 sources: profiles/r04_ragged_ab.txt)
+    const int64_t w = W <= 2 ? int64_t(blockIdx.x) : xcd_work_index(total);
     const int o = ragged_find(objs, n, w, false);
     const RaggedObj &d = objs[o];
     const int64_t l = w - d.wg0;
     const int rt = int(l % d.row_tiles), cb = int(l / d.row_tiles);
     const MatmulParams q = ragged_params(d);
-    bsj_tile<W, true, false>(q, stream + d.idx0, d.row_tiles, rt, cb, 0, 1u, nullptr);
+    bsj_tile<W, (W >= 4), false>(q, stream + d.idx0, d.row_tiles, rt, cb, 0, 1u, nullptr);
 }
 
 // tails and shapes the bit-sliced program does not take: the perm kernel's tile on one object (byte-granular
@@ -832,17 +840,113 @@ __device__ __forceinline__ void perm_ragged_tile(const MatmulParams &q, int rt, 
     copy_header(q, t);
 }
 
+// A partial column block (the < 4 KiB tail of an object -- a recode's k coefficient bytes after its bit-sliced
+// blocks, a narrow piece): S = ceil(bytes / 16) slots, so a one-lane-per-slot tile leaves most of the workgroup idle
+// and walks all n_in sources one dependent load after another (~1 us each: 124 us for the 130-source recode tails of
+// scripts/ragged_rate.py).  Here the sources are split over G = min(256 / S2, 32) lane groups (S2 = S rounded up to a
+// power of two): group g takes sources g, g + G, ... with PF rows in flight, each lane builds the perm tables of its
+// (row, source) coefficients in registers (no LDS table chunks, no barriers in the loop), and the G partial products
+// are XOR-reduced through LDS.
+template <bool AL>
+__device__ __forceinline__ void perm_ragged_split_tile(const MatmulParams &q, int rt, int cb, uint4 *red) {
+    constexpr int NT = kRaggedPermRows, PF = 4;
+    const int tid = threadIdx.x;
+    const int64_t c0 = int64_t(cb) * kColBlock;
+    const int S = int((min<int64_t>(kColBlock, q.width - c0) + 15) / 16);
+    int lg = 0;
+    while ((1 << lg) < S) ++lg;
+    const int S2 = 1 << lg, G = min(kThreads >> lg, 32);
+    const int slot = tid & (S2 - 1), g = tid >> lg;
+    const int row0 = rt * NT, rows_here = min(NT, q.n_out - row0);
+    const int64_t col = c0 + int64_t(slot) * kBytesPerThread;
+    const int nbytes = (g < G && slot < S) ? int(min<int64_t>(kBytesPerThread, q.width - col)) : 0;
+    const uint8_t *coef_base = q.coef + int64_t(row0) * q.coef_row;
+    uint32_t acc[NT][4];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i][0] = acc[i][1] = acc[i][2] = acc[i][3] = 0u;
+    if (nbytes > 0) {
+        const uint8_t *in = q.in + col;
+        for (int j0 = g; j0 < q.n_in; j0 += G * PF) {
+            uint4 x[PF];
+#pragma unroll
+            for (int u = 0; u < PF; ++u)  // clamped: past n_in re-read the last source (its product is skipped)
+                x[u] = load16<AL>(in + int64_t(min(j0 + u * G, q.n_in - 1)) * q.in_row, nbytes);
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                const int j = j0 + u * G;
+                if (j >= q.n_in) break;
+                const Sel a = selectors(x[u]);
+#pragma unroll
+                for (int i = 0; i < NT; ++i) {
+                    if (i >= rows_here) break;
+                    uint32_t t0lo, t0hi, t1lo, t1hi, t2;
+                    perm_table_regs(coef_base[int64_t(i) * q.coef_row + j], t0lo, t0hi, t1lo, t1hi, t2);
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq)
+                        acc[i][qq] = xor3(xor3(acc[i][qq], vperm(t0hi, t0lo, a.s0[qq]), vperm(t1hi, t1lo, a.s1[qq])),
+                                          vperm(t2, t2, a.s2[qq]), 0u);
+                }
+            }
+        }
+    }
+    if (G > 1) {  // red[i][g][slot]: the G partials of row i, slot
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+            if (g < G) red[(i * G + g) * S2 + slot] = make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+        __syncthreads();
+    }
+    // output (row i, slot): one lane each, XOR of its G partials
+    for (int e = tid; e < NT * S2; e += kThreads) {
+        const int i = e >> lg, sl = e & (S2 - 1);
+        if (i >= rows_here || sl >= S) continue;
+        const int64_t oc = c0 + int64_t(sl) * kBytesPerThread;
+        const int nb = int(min<int64_t>(kBytesPerThread, q.width - oc));
+        uint4 v;
+        if (G > 1) {
+            v = red[(i * G) * S2 + sl];
+            for (int gg = 1; gg < G; ++gg) {
+                const uint4 r = red[(i * G + gg) * S2 + sl];
+                v.x ^= r.x;
+                v.y ^= r.y;
+                v.z ^= r.z;
+                v.w ^= r.w;
+            }
+        } else {  // G = 1 (S2 = 256): lane e = slot e holds row i's product itself
+            v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int ii = 0; ii < NT; ++ii)
+                if (ii == i) v = make_uint4(acc[ii][0], acc[ii][1], acc[ii][2], acc[ii][3]);
+        }
+        store16<AL>(q.out + int64_t(row0 + i) * q.out_row + oc, v, nb);
+    }
+    Tile t;
+    t.obj = 0;
+    t.cb = cb;
+    t.row0 = row0;
+    t.rows_here = rows_here;
+    copy_header(q, t);
+}
+
 __global__ __launch_bounds__(kThreads) void gf_matmul_perm_ragged_kernel(const RaggedObj *objs, int n, int64_t total) {
+    // the split tile's partials: NT rows x 256 lanes x 16 bytes at most (G x S2 <= 256)
+    __shared__ uint4 red[kRaggedPermRows * kThreads];
     const int64_t w = xcd_work_index(total);
     const int o = ragged_find(objs, n, w, false);
     const RaggedObj &d = objs[o];
     const int64_t l = w - d.wg0;
     const int rt = int(l % d.row_tiles), cb = int(l / d.row_tiles);
     const MatmulParams q = ragged_params(d);
-    if (d.aligned)
+    const bool partial = q.width - int64_t(cb) * kColBlock < kColBlock;  // workgroup-uniform
+    if (partial) {
+        if (d.aligned)
+            perm_ragged_split_tile<true>(q, rt, cb, red);
+        else
+            perm_ragged_split_tile<false>(q, rt, cb, red);
+    } else if (d.aligned) {
         perm_ragged_tile<true>(q, rt, cb);
-    else
+    } else {
         perm_ragged_tile<false>(q, rt, cb);
+    }
 }
 
 // strided row copy (the coded pieces' coefficient headers, encoder.rs:246-248): one byte per thread
@@ -1322,13 +1426,13 @@ __attribute__((weak)) hipError_t launch_matmul_ab(const MatmulParams &, hipStrea
 __attribute__((weak)) size_t matmul_scratch_bytes_ab(const MatmulParams &, MatmulVariant) { return 0; }
 
 bool ragged_bsj_eligible(const uint8_t *in, const uint8_t *out, int64_t in_row, int64_t out_row, int64_t width,
-                         int n_out) {
-    return (unaligned_vector_ok() || (al16(in) && al16(out) && al16(in_row) && al16(out_row))) && width >= kBsjColBlock &&
+                         int n_out, bool unaligned_ok) {
+    return (unaligned_ok || (al16(in) && al16(out) && al16(in_row) && al16(out_row))) && width >= kBsjColBlock &&
            n_out >= 4 &&
            in_row < (int64_t(1) << 32) && out_row < (int64_t(1) << 32);
 }
 
-int ragged_bsj_waves(int n_out) { return n_out > 32 ? 8 : 4; }
+int ragged_bsj_waves(int n_out) { return n_out > 32 ? 8 : bsj_waves(n_out); }
 
 hipError_t ragged_bsj_base(hipStream_t s, void *probe_scratch, uint64_t &base) {
     return bsj_shared_base(s, probe_scratch, base);
@@ -1351,6 +1455,10 @@ hipError_t launch_ragged_bsj(int W, const RaggedObj *objs, int n, int64_t wgs, c
         hipLaunchKernelGGL(gf_matmul_bsj_ragged_kernel<8>, dim3(unsigned(wgs)), dim3(512), 0, s, objs, n, wgs, st);
     else if (W == 4)
         hipLaunchKernelGGL(gf_matmul_bsj_ragged_kernel<4>, dim3(unsigned(wgs)), dim3(256), 0, s, objs, n, wgs, st);
+    else if (W == 2)
+        hipLaunchKernelGGL(gf_matmul_bsj_ragged_kernel<2>, dim3(unsigned(wgs)), dim3(128), 0, s, objs, n, wgs, st);
+    else if (W == 1)
+        hipLaunchKernelGGL(gf_matmul_bsj_ragged_kernel<1>, dim3(unsigned(wgs)), dim3(64), 0, s, objs, n, wgs, st);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();

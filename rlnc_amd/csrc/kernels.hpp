@@ -103,8 +103,9 @@ constexpr int kRaggedPermRows = 8;     // output rows per workgroup of the ragge
 constexpr int kRaggedColBlock = 4096;  // columns per workgroup (both ragged kernels)
 // the bit-sliced program takes whole 4 KiB column blocks of 16-byte-aligned operands with >= 4 output rows
 bool ragged_bsj_eligible(const uint8_t *in, const uint8_t *out, int64_t in_row, int64_t out_row, int64_t width,
-                         int n_out);
-int ragged_bsj_waves(int n_out);  // 4 (32-row tiles) up to 32 output rows, else 8 (64-row tiles)
+                         int n_out,
+                         bool unaligned_ok);  // unaligned_ok: unaligned_vector_ok(), looked up once per call
+int ragged_bsj_waves(int n_out);  // 1, 2, 4 waves (8, 16, 32-row tiles) up to 32 output rows, else 8 (64-row tiles)
 // the shared program's block table address (probe_scratch: >= 8 device bytes; synchronous the first time)
 hipError_t ragged_bsj_base(hipStream_t s, void *probe_scratch, uint64_t &base);
 hipError_t launch_ragged_offsets(const RaggedObj *objs, int n, int64_t entries, void *stream, uint64_t base,

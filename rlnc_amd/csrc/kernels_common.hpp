@@ -24,6 +24,22 @@ __device__ __forceinline__ uint32_t vperm(uint32_t hi, uint32_t lo, uint32_t sel
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
 
+// make_perm_table (gf256.hpp) in registers: T0[v] = c·v is linear in the bits of v, so with m_b = c·2^b the
+// low dword's bytes are {0, m0, m1, m0^m1} and the high dword's are the low ones XOR m2 (likewise T1 from m3..m5,
+// T2 = {0, m6, m7, m6^m7})
+__device__ __forceinline__ void perm_table_regs(uint32_t c, uint32_t &t0lo, uint32_t &t0hi, uint32_t &t1lo,
+                                                uint32_t &t1hi, uint32_t &t2) {
+    uint32_t m[8];
+    m[0] = c;
+#pragma unroll
+    for (int b = 1; b < 8; ++b) m[b] = ((m[b - 1] << 1) ^ ((m[b - 1] & 0x80u) ? 0x1Bu : 0u)) & 0xFFu;
+    t0lo = (m[0] << 8) | (m[1] << 16) | ((m[0] ^ m[1]) << 24);
+    t0hi = t0lo ^ (m[2] * 0x01010101u);
+    t1lo = (m[3] << 8) | (m[4] << 16) | ((m[3] ^ m[4]) << 24);
+    t1hi = t1lo ^ (m[5] * 0x01010101u);
+    t2 = (m[6] << 8) | (m[7] << 16) | ((m[6] ^ m[7]) << 24);
+}
+
 template <bool ALIGNED>
 __device__ __forceinline__ uint4 load16(const uint8_t *p, int nbytes) {
     if (ALIGNED && nbytes == 16) return *reinterpret_cast<const uint4 *>(p);

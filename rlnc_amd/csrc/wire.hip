@@ -39,6 +39,14 @@ __global__ __launch_bounds__(256) void table_fill_kernel(uint8_t *dst, TableChun
     for (uint32_t i = threadIdx.x; i < c.bytes; i += 256) dst[i] = c.data[i];
 }
 
+// eager upload: the device reads the pinned staging buffer itself (one load per thread in flight across PCIe),
+// instead of a hipMemcpyAsync host-to-device copy, whose DMA set-up put ~60 us ahead of the first kernel of a
+// 256-object ragged recode (scripts/ragged_rate.py)
+__global__ __launch_bounds__(256) void table_copy_kernel(uint4 *dst, const uint4 *src, uint32_t n16) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n16) dst[i] = src[i];
+}
+
 int upload_table(rlnc_context *ctx, const void *host, size_t bytes, void **dev) {
     const size_t need = round16(std::max<size_t>(bytes, 16));
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -75,12 +83,20 @@ int upload_table(rlnc_context *ctx, const void *host, size_t bytes, void **dev) 
         }
     }
     int st;
-    if (ctx->tab_ev) HIP_TRY(hipEventSynchronize(ctx->tab_ev));
-    if ((st = ctx->grow(ctx->pin_tab, need)) || (st = ctx->grow(ctx->ws_tab, need))) return st;
-    std::memcpy(ctx->pin_tab.p, host, bytes);
-    HIP_TRY(hipMemcpyAsync(ctx->ws_tab.p, ctx->pin_tab.p, bytes, hipMemcpyHostToDevice, ctx->stream));
-    if (!ctx->tab_ev) HIP_TRY(hipEventCreateWithFlags(&ctx->tab_ev, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(ctx->tab_ev, ctx->stream));
+    const int r = ctx->tab_next;
+    ctx->tab_next = (r + 1) % rlnc_context::kTabRing;
+    PinBuf &pin = ctx->pin_tab[r];
+    hipEvent_t &ev = ctx->tab_ev[r];
+    if (ev) HIP_TRY(hipEventSynchronize(ev));
+    if ((st = ctx->grow(pin, need)) || (st = ctx->grow(ctx->ws_tab, need))) return st;
+    std::memcpy(pin.p, host, bytes);
+    if (need / 16 > 0xFFFFFF00u) return set_error(RLNC_ERR_INVALID_ARGUMENT, "descriptor table too large");
+    const uint32_t n16 = uint32_t(need / 16);
+    hipLaunchKernelGGL(table_copy_kernel, dim3((n16 + 255) / 256), dim3(256), 0, ctx->stream,
+                       static_cast<uint4 *>(ctx->ws_tab.p), static_cast<const uint4 *>(pin.p), n16);
+    HIP_TRY(hipGetLastError());
+    if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ev, ctx->stream));
     *dev = ctx->ws_tab.p;
     return RLNC_OK;
 }
@@ -149,10 +165,10 @@ int pad_check(const rlnc_pad_desc &d, PadDesc &o) {
 // ---------------------------------------------------------------------------------------------------------------
 // Ragged matmul: Out_o = Coef_o ⊗ In_o for objects of any shapes, one launch per kernel stage.  Each object's whole
 // 4 KiB column blocks go to the bit-sliced program (the hot path of the uniform batches, §4.1 of DESIGN.md) -- one
-// launch for objects of <= 32 output rows (4-wave, 32-row tiles) and one for larger ones (8-wave, 64-row tiles), after
-// ONE launch that writes every object's block-address stream -- and whatever it does not take (the ragged < 4 KiB
-// tail, unaligned operands, < 4 output rows) to one launch of the perm kernel.  So at most 4 launches, whatever the
-// number of objects and shapes.
+// launch per tile class: 1, 2 and 4 waves (8-, 16- and 32-row tiles, as the uniform product sizes its tiles) for
+// objects of <= 8, <= 16 and <= 32 output rows, 8 waves (64-row tiles) above -- after ONE launch that writes every
+// object's block-address stream, and whatever it does not take (the ragged < 4 KiB tail, unaligned operands, < 4
+// output rows) to one launch of the perm kernel.  So at most 6 launches, whatever the number of objects and shapes.
 // ---------------------------------------------------------------------------------------------------------------
 struct MatmulJob {
     const uint8_t *in, *coef;
@@ -165,14 +181,15 @@ bool al16p(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 int ragged_matmul(rlnc_context *ctx, const std::vector<MatmulJob> &jobs) {
     using rlnc::RaggedObj;
-    std::vector<RaggedObj> w4, w8, perm;
-    // the bit-sliced program needs its block table's address (one probe per device, synchronous the first time;
-    // inside a capture that first probe cannot run: everything then takes the perm kernel, bit-identical)
+    std::vector<RaggedObj> cls[4], perm;  // bit-sliced classes of 1, 2, 4, 8 waves
+    // the shared-set bit-sliced programs need their block table's address (one probe per device, synchronous the first
+    // time; inside a capture that first probe cannot run: their objects then take the perm kernel, bit-identical)
     uint64_t base = 0;
     bool any_bsj = false;
+    const bool uv = rlnc::unaligned_vector_ok();  // once per call: hipGetDevice per object was ~0.1 us each
     for (const auto &j : jobs)
         any_bsj |= j.n_out > 0 && j.n_in > 0 && j.width > 0 &&
-                   rlnc::ragged_bsj_eligible(j.in, j.out, j.in_row, j.out_row, j.width, j.n_out);
+                   rlnc::ragged_bsj_eligible(j.in, j.out, j.in_row, j.out_row, j.width, j.n_out, uv);
     int st;
     if (any_bsj) {
         if ((st = ctx->grow(ctx->ws_idx, 512))) return st;
@@ -181,7 +198,9 @@ int ragged_matmul(rlnc_context *ctx, const std::vector<MatmulJob> &jobs) {
     for (const auto &j : jobs) {
         if (j.n_out <= 0 || j.n_in <= 0 || j.width <= 0) continue;
         int64_t full = 0;
-        if (base != 0 && rlnc::ragged_bsj_eligible(j.in, j.out, j.in_row, j.out_row, j.width, j.n_out)) {
+        // (the 1- and 2-wave programs take block offsets, not addresses: no base needed)
+        if ((base != 0 || rlnc::ragged_bsj_waves(j.n_out) <= 2) &&
+            rlnc::ragged_bsj_eligible(j.in, j.out, j.in_row, j.out_row, j.width, j.n_out, uv)) {
             full = (j.width / rlnc::kRaggedColBlock) * rlnc::kRaggedColBlock;
             const int W = rlnc::ragged_bsj_waves(j.n_out);
             RaggedObj d{};
@@ -200,7 +219,7 @@ int ragged_matmul(rlnc_context *ctx, const std::vector<MatmulJob> &jobs) {
             d.tile_rows = 8 * W;
             d.row_tiles = (j.n_out + d.tile_rows - 1) / d.tile_rows;
             d.col_blocks = int(full / rlnc::kRaggedColBlock);
-            (W == 8 ? w8 : w4).push_back(d);
+            cls[W == 8 ? 3 : W == 4 ? 2 : W - 1].push_back(d);
         }
         if (full < j.width) {
             RaggedObj d{};
@@ -218,24 +237,31 @@ int ragged_matmul(rlnc_context *ctx, const std::vector<MatmulJob> &jobs) {
             d.n_in = j.n_in;
             d.row_tiles = (j.n_out + rlnc::kRaggedPermRows - 1) / rlnc::kRaggedPermRows;
             d.col_blocks = int((d.width + rlnc::kRaggedColBlock - 1) / rlnc::kRaggedColBlock);
-            d.aligned = rlnc::unaligned_vector_ok() ||
+            d.aligned = uv ||
                         (al16p(j.in + full) && al16p(j.out + full) && (j.in_row & 15) == 0 && (j.out_row & 15) == 0);
             perm.push_back(d);
         }
     }
-    const size_t n4 = w4.size(), n8 = w8.size(), np = perm.size();
-    if (n4 + n8 + np == 0) return RLNC_OK;
-    if (n4 + n8 + np > 0x7FFFFFFF) return set_error(RLNC_ERR_INVALID_ARGUMENT, "ragged batch too large");
-    // table: [4-wave bit-sliced][8-wave bit-sliced][perm]; wg0 numbered per launch, idx0 across both bit-sliced ones
+    size_t nb = 0;
+    for (auto &v : cls) nb += v.size();
+    // the 1- and 2-wave classes by source count, most first (a workgroup's time is about its source count; their
+    // kernel launches the tiles in table order: gf_matmul_bsj_ragged_kernel)
+    for (int c = 0; c < 2; ++c)
+        std::stable_sort(cls[c].begin(), cls[c].end(),
+                         [](const RaggedObj &a, const RaggedObj &b) { return a.n_in > b.n_in; });
+    const size_t np = perm.size();
+    if (nb + np == 0) return RLNC_OK;
+    if (nb + np > 0x7FFFFFFF) return set_error(RLNC_ERR_INVALID_ARGUMENT, "ragged batch too large");
+    // table: [1-wave][2-wave][4-wave][8-wave bit-sliced][perm]; wg0 numbered per launch, idx0 (8-byte units) across
+    // all the bit-sliced classes
     std::vector<RaggedObj> tab;
-    tab.reserve(n4 + n8 + np);
-    int64_t idx = 0, wg4 = 0, wg8 = 0, wgp = 0;
-    for (auto *v : {&w4, &w8})
-        for (auto &d : *v) {
-            int64_t &wg = v == &w4 ? wg4 : wg8;
-            d.wg0 = wg;
+    tab.reserve(nb + np);
+    int64_t idx = 0, wgc[4] = {0, 0, 0, 0}, wgp = 0;
+    for (int c = 0; c < 4; ++c)
+        for (auto &d : cls[c]) {
+            d.wg0 = wgc[c];
             d.idx0 = idx;
-            wg += int64_t(d.row_tiles) * d.col_blocks;
+            wgc[c] += int64_t(d.row_tiles) * d.col_blocks;
             idx += int64_t(d.row_tiles) * d.n_in * d.tile_rows;
             tab.push_back(d);
         }
@@ -244,16 +270,19 @@ int ragged_matmul(rlnc_context *ctx, const std::vector<MatmulJob> &jobs) {
         wgp += int64_t(d.row_tiles) * d.col_blocks;
         tab.push_back(d);
     }
-    if (wg4 > 0x7FFFFFFF || wg8 > 0x7FFFFFFF || wgp > 0x7FFFFFFF)
+    if (std::max({wgc[0], wgc[1], wgc[2], wgc[3], wgp}) > 0x7FFFFFFF)
         return set_error(RLNC_ERR_INVALID_ARGUMENT, "ragged batch too large for one launch");
     if (idx > 0 && (st = ctx->grow(ctx->ws_idx, size_t(idx) * 8 + 512))) return st;
     void *dtab = nullptr;
     if ((st = upload_table(ctx, tab.data(), tab.size() * sizeof(RaggedObj), &dtab))) return st;
     const RaggedObj *t = static_cast<const RaggedObj *>(dtab);
-    HIP_TRY(rlnc::launch_ragged_offsets(t, int(n4 + n8), idx, ctx->ws_idx.p, base, ctx->stream));
-    HIP_TRY(rlnc::launch_ragged_bsj(4, t, int(n4), wg4, ctx->ws_idx.p, ctx->stream));
-    HIP_TRY(rlnc::launch_ragged_bsj(8, t + n4, int(n8), wg8, ctx->ws_idx.p, ctx->stream));
-    HIP_TRY(rlnc::launch_ragged_perm(t + n4 + n8, int(np), wgp, ctx->stream));
+    HIP_TRY(rlnc::launch_ragged_offsets(t, int(nb), idx, ctx->ws_idx.p, base, ctx->stream));
+    size_t at = 0;
+    for (int c = 0; c < 4; ++c) {
+        HIP_TRY(rlnc::launch_ragged_bsj(1 << c, t + at, int(cls[c].size()), wgc[c], ctx->ws_idx.p, ctx->stream));
+        at += cls[c].size();
+    }
+    HIP_TRY(rlnc::launch_ragged_perm(t + nb, int(np), wgp, ctx->stream));
     return RLNC_OK;
 }
 
