@@ -34,7 +34,8 @@ __device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stre
     // W = 8: one workgroup per CU, so a deeper ring and 2 BAR8 set slots (the builders run BAR8 rows ahead); W = 1:
     // a deeper ring too (its one wave alone keeps the source rows in flight)
     __shared__ __attribute__((aligned(16))) uint8_t
-        ring[(W == 8 ? RLNC_BSJ_SLOTS8 : W == 1 ? RLNC_BSJ_SLOTS1 : RLNC_BSJ_SLOTS) * kBsjColBlock];
+        ring[(W == 8 ? RLNC_BSJ_SLOTS8 : W == 1 ? RLNC_BSJ_SLOTS1 : W == 2 ? RLNC_BSJ_SLOTS2 : RLNC_BSJ_SLOTS) *
+             kBsjColBlock];
     __shared__ __attribute__((aligned(16))) uint8_t cset[SHARE ? (W == 8 ? RLNC_BSJ_CSET_BYTES8 : RLNC_BSJ_CSET_BYTES) : 16];
     const int row0 = rt * kTileRows;
     const int rows = min(kTileRows, p.n_out - row0);

@@ -101,7 +101,7 @@ struct PinBuf {
 struct CallWs {
     hipStream_t stream = nullptr;
     hipEvent_t ev = nullptr;
-    DevBuf coef, out, idx, scan, status, len;
+    DevBuf coef, out, idx, status, len;
     PinBuf pin_a, pin_b, pin_c;
     // the call-latency kernel (piece.hip): coefficients read and output rows written by the kernel in host memory,
     // per-chunk completion flags raised to the call's epoch, and the chunks' workgroup counters on the device
@@ -190,7 +190,7 @@ struct rlnc_context {
                           // 3 device elimination with the clean state on LDS, 4 ... on one wave's
                           // registers, 5 blocked clean run, 6 round-1 multi-wave registers (A/B)
     // workspaces of the stream-ordered batch / _device API (one caller thread per context at a time)
-    DevBuf ws_coef, ws_out, ws_scan, ws_status, ws_len, ws_pstat, ws_rank, ws_idx;
+    DevBuf ws_coef, ws_out, ws_status, ws_len, ws_pstat, ws_rank, ws_idx;
     PinBuf pin_a, pin_b, pin_c;
     // set once a batch call ran inside a HIP stream capture: the graph holds the workspace addresses, so
     // they must never move again (grow() refuses instead of reallocating)

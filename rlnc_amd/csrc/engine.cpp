@@ -980,12 +980,11 @@ int rlnc_decoder_get_decoded_data_device(rlnc_decoder *d, uint8_t *out_dev, size
     Lease ws(d->ctx);
     if ((st = ws.acquire())) return st;
     if ((st = decoder_apply(d, ws.ws.get(), out_dev))) return st;
-    if ((st = ws->scan.ensure(8)) || (st = ws->status.ensure(4)) || (st = ws->len.ensure(8)) ||
+    if ((st = ws->status.ensure(4)) || (st = ws->len.ensure(8)) ||
         (st = ws->pin_c.ensure(16)))
         return st;
-    HIP_TRY(rlnc::launch_final_data_len(out_dev, 0, int64_t(d->k * d->L), 1, ws->scan.as<unsigned long long>(),
-                                        ws->status.as<int32_t>(), ws->len.as<int64_t>(),
-                                        RLNC_ERR_INVALID_DECODED_DATA_FORMAT, ws->stream));
+    HIP_TRY(rlnc::launch_final_data_len(out_dev, 0, int64_t(d->k * d->L), 1, ws->status.as<int32_t>(),
+                                        ws->len.as<int64_t>(), RLNC_ERR_INVALID_DECODED_DATA_FORMAT, ws->stream));
     HIP_TRY(hipMemcpyAsync(ws->pin_c.p, ws->status.p, 4, hipMemcpyDeviceToHost, ws->stream));
     HIP_TRY(hipMemcpyAsync(ws->pin_c.as<uint8_t>() + 8, ws->len.p, 8, hipMemcpyDeviceToHost, ws->stream));
     HIP_TRY(hipStreamSynchronize(ws->stream));
@@ -1113,7 +1112,6 @@ static int decode_apply_impl(rlnc_context *ctx, const uint8_t *pieces, size_t ob
                              int32_t *ostat_dev, int64_t *len_dev) {
     const size_t full = k + L;
     int st;
-    if ((st = ctx->grow(ctx->ws_scan, nobj * 8))) return st;
     rlnc::MatmulParams p{};
     p.in = pieces + k;
     p.in_obj = int64_t(obj_stride);
@@ -1130,7 +1128,7 @@ static int decode_apply_impl(rlnc_context *ctx, const uint8_t *pieces, size_t ob
     p.n_obj = int(nobj);
     if ((st = ctx->matmul(p))) return st;
     HIP_TRY(rlnc::launch_final_data_len_ranked(decoded, int64_t(k * L), int64_t(k * L), int(nobj), int(k), rank_dev,
-                                               ctx->ws_scan.as<unsigned long long>(), ostat_dev, len_dev, ctx->stream));
+                                               ostat_dev, len_dev, ctx->stream));
     return RLNC_OK;
 }
 
@@ -1197,7 +1195,7 @@ static int decode_batch_host_impl(rlnc_context *ctx, const uint8_t *pieces, size
     }
     // 3. T → device, decoded = T × received data rows (one launch for all objects)
     if ((st = ctx->grow(ctx->ws_coef, nobj * k * m)) || (st = ctx->grow(ctx->ws_rank, nobj * 4)) ||
-        (st = ctx->grow(ctx->ws_scan, nobj * 8)) || (st = ctx->grow(ctx->ws_status, nobj * 4)) ||
+        (st = ctx->grow(ctx->ws_status, nobj * 4)) ||
         (st = ctx->grow(ctx->ws_len, nobj * 8)) || (st = ctx->grow(ctx->pin_c, nobj * 16)))
         return st;
     HIP_TRY(hipMemcpyAsync(ctx->ws_coef.p, T, nobj * k * m, hipMemcpyHostToDevice, ctx->stream));
@@ -1219,8 +1217,8 @@ static int decode_batch_host_impl(rlnc_context *ctx, const uint8_t *pieces, size
     if ((st = ctx->matmul(p))) return st;
     // 4. get_final_data_len on device (decoder.rs:162-177)
     HIP_TRY(rlnc::launch_final_data_len_ranked(decoded, int64_t(k * L), int64_t(k * L), int(nobj), int(k),
-                                               ctx->ws_rank.as<int32_t>(), ctx->ws_scan.as<unsigned long long>(),
-                                               ctx->ws_status.as<int32_t>(), ctx->ws_len.as<int64_t>(), ctx->stream));
+                                               ctx->ws_rank.as<int32_t>(), ctx->ws_status.as<int32_t>(),
+                                               ctx->ws_len.as<int64_t>(), ctx->stream));
     int32_t *hst = ctx->pin_c.as<int32_t>();
     int64_t *hlen = reinterpret_cast<int64_t *>(ctx->pin_c.as<uint8_t>() + nobj * 8);
     HIP_TRY(hipMemcpyAsync(hst, ctx->ws_status.p, nobj * 4, hipMemcpyDeviceToHost, ctx->stream));

@@ -905,6 +905,7 @@ def main():
     # (0.2228 / 0.2205 ms against 0.2188 / 0.2233, profiles/r04_ragged_ab.txt): the 1-wave program is not waiting on
     # its source rows there
     ap.add_argument("--slots1", type=int, default=3, help="ring slots of the 1-wave program (3 = the 2-row form)")
+    ap.add_argument("--slots2", type=int, default=3, help="ring slots of the 2-wave program (3 = the 2-row form)")
     ap.add_argument("--store-hint", default="", help="cache-policy modifiers of the tile stores, e.g. 'nt' (A/B)")
     args = ap.parse_args()
     HINTS["load"], HINTS["store"] = args.load_hint, args.store_hint
@@ -930,10 +931,11 @@ def main():
         f.write(f"#define RLNC_BSJ_SLOTS {SLOTS}\n")
         f.write(f"#define RLNC_BSJ_BLOCK_BYTES {BLOCK_BYTES}\n")
         f.write(f"#define RLNC_BSJ_SLOTS1 {args.slots1}\n")
+        f.write(f"#define RLNC_BSJ_SLOTS2 {args.slots2}\n")
         for w in (1, 2, 4):
             WAVES, WG_ROWS = w, NT * w
             STREAM_J_BYTES = WG_ROWS * 4
-            body_txt = "\\n\\t".join(hinted(program(args.slots1 if w == 1 else SLOTS)))
+            body_txt = "\\n\\t".join(hinted(program({1: args.slots1, 2: args.slots2}.get(w, SLOTS))))
             f.write(f'#define RLNC_BSJ_ASM_W{w} "{body_txt}"\n')
         WAVES, WG_ROWS = 4, NT * 4
         STREAM_J_BYTES = WG_ROWS * 8  # 64-bit block addresses

@@ -122,11 +122,9 @@ hipError_t launch_copy_rows(uint8_t *dst, int64_t dst_stride, const uint8_t *src
 hipError_t launch_mul_add(uint8_t *dst, const uint8_t *src, int64_t len, uint8_t scalar, hipStream_t s);
 
 // decoder.rs:162-177 on device, per object: finds the last nonzero byte of the padded payload
-// data[o][0:len); status[o] = 0 / InvalidDecodedDataFormat code, final_len[o] = marker index.
-// `scratch` holds n_obj uint64 words.
-hipError_t launch_final_data_len(const uint8_t *data, int64_t obj_stride, int64_t len, int n_obj,
-                                 unsigned long long *scratch, int32_t *status, int64_t *final_len,
-                                 int32_t invalid_code, hipStream_t s);
+// data[o][0:len); status[o] = 0 / invalid_code, final_len[o] = marker index (one launch, one wave per object).
+hipError_t launch_final_data_len(const uint8_t *data, int64_t obj_stride, int64_t len, int n_obj, int32_t *status,
+                                 int64_t *final_len, int32_t invalid_code, hipStream_t s);
 
 // Device replica of Decoder::decode over pieces 0..m-1 of every object (rref.hip).  Piece p of object o
 // starts (coefficient header first) at pieces + o*obj_stride + p*piece_stride.  Outputs: status[o][p]
@@ -173,7 +171,6 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s);
 
 // final_len with the decoder's rank: objects with rank < k report NotAllPiecesReceivedYet
 hipError_t launch_final_data_len_ranked(const uint8_t *data, int64_t obj_stride, int64_t len, int n_obj, int k,
-                                        const int32_t *rank, unsigned long long *scratch, int32_t *status,
-                                        int64_t *final_len, hipStream_t s);
+                                        const int32_t *rank, int32_t *status, int64_t *final_len, hipStream_t s);
 
 }  // namespace rlnc
