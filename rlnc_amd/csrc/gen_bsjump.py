@@ -652,8 +652,8 @@ def body_s8(L, j):
         L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 24f", "s_waitcnt vmcnt(1)", "24:", "s_waitcnt lgkmcnt(0)"]
     else:
         L.append("s_waitcnt vmcnt(1) lgkmcnt(0)")  # rows <= j+DMA8-2 landed; own LDS ops + addresses done
-    if j % BAR8 == 0:
-        L.append("s_barrier")
+    if j % BAR8 == 0:  # --diag=s8nobar: no barrier in the loop at all (timing only, wrong results): the most any
+        L.append("s_barrier" if "s8nobar" not in DIAG else "s_nop 0")  # barrier replacement could gain
     L.append(f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1")
     if PRIO8 is not None:
         L.append("s_setprio 0")
