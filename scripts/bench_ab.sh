@@ -9,6 +9,6 @@ for rep in 1 2; do
     # exit 3 = verification failed: expected of the timing-only diagnostic builds (their JSON line is still printed)
     out=$(env ${envs//,/ } timeout -k 10 200 python bench.py --no-cpu-baseline ${args//,/ } 2>/dev/null)
     rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 3 ]; then echo "$label failed ($rc)"; exit 1; fi
-    echo "$out" | python -c "import json,sys; d=json.loads([l for l in sys.stdin.read().splitlines() if l.startswith('{')][-1]); print('$label', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], 'verified' if d.get('verified', d.get('breakdown', {}).get('verified')) else 'NOT-verified')"
+    echo "$out" | python -c "import json,sys; d=json.loads([l for l in sys.stdin.read().splitlines() if l.startswith('{')][-1]); print('$label', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], 'decode_ms', d.get('breakdown', {}).get('decode_ms'), 'verified' if d.get('verified', d.get('breakdown', {}).get('verified')) else 'NOT-verified')"
   done
 done
