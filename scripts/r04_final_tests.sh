@@ -1,0 +1,7 @@
+# round-4 final: the whole -m gpu suite on the shipped library, then the A/B build's variant tests
+set -o pipefail
+mkdir -p gpurun_out/final
+timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/final/gpu_tests.log 2>&1 || { tail -40 gpurun_out/final/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/final/gpu_tests.log
+RLNC_LIB_PATH=$PWD/rlnc_amd/librlnc_hip_ab.so timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_fullrange.py tests/test_gpu_graph.py > gpurun_out/final/ab_tests.log 2>&1 || { tail -40 gpurun_out/final/ab_tests.log; exit 1; }
+tail -2 gpurun_out/final/ab_tests.log
