@@ -122,10 +122,11 @@ def test_recode_with_buf_matches_oracle(ctx, orc, size, k):
 
 
 @pytest.mark.parametrize("size,k", [(1 << 20, 16), (1 << 20, 32), (1 << 20, 128), (1 << 20, 256), (1 << 24, 16),
-                                    (1 << 24, 32), (3000, 5)])
+                                    (1 << 24, 32), ((1 << 25) + 12345, 64), (3000, 5)])
 def test_get_decoded_data_recovers_source(ctx, size, k):
     """The decoder's T x data product through the piece kernel (k output rows, one flag chunk per 64 KiB of a row)
-    returns the source bytes (decoder.rs:136-177), with dependent pieces mixed in."""
+    returns the source bytes (decoder.rs:136-177), with dependent pieces mixed in.  Objects above 4 MiB take the batch
+    kernels and one device-to-host copy."""
     from rlnc_amd.full import Decoder, Encoder
 
     rng = np.random.default_rng(size + 3 * k)
