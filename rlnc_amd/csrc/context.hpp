@@ -140,7 +140,8 @@ struct UpSlot {
 // context had then): the block may be reused by another object only after the last of them.  Synchronous uses (the
 // object API on host buffers, the decoder's uploads) are complete when their call returns and need no record.
 struct ObjUse {
-    hipEvent_t ev = nullptr;  // recorded after the latest stream-ordered use
+    hipEvent_t ev = nullptr;  // recorded after the latest stream-ordered use, and after every earlier one
+    hipStream_t last = nullptr;
     bool used = false;
     bool captured = false;  // a use inside a HIP graph capture: the graph may replay it at any time
     ~ObjUse() {
@@ -154,7 +155,11 @@ struct ObjUse {
             return RLNC_OK;
         }
         if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        // a use on another stream than the previous one: the event re-recorded on s must still follow that earlier
+        // use (it may run after this one), so s waits for the event's previous recording first
+        if (used && s != last) HIP_TRY(hipStreamWaitEvent(s, ev, 0));
         HIP_TRY(hipEventRecord(ev, s));
+        last = s;
         used = true;
         return RLNC_OK;
     }

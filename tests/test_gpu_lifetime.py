@@ -102,3 +102,44 @@ def test_dropped_encoder_block_reused_only_after_its_launches():
     want = orc.encode(data.reshape(k, L), coeffs)
     assert np.array_equal(got, want)
     del enc2, keep
+
+
+def test_block_reused_only_after_uses_on_two_streams():
+    """An encoder used on stream A (behind ~40 ms of other work) and then on stream B (nothing ahead): dropping it
+    must wait for A's launch too, not only for the latest use on B, before the block cache hands the block to a new
+    encoder whose upload overwrites the source."""
+    import torch
+
+    import rlnc_amd
+    from oracle.oracle import Oracle, build
+    from rlnc_amd.full import Encoder
+
+    build()
+    orc = Oracle()
+    ctx = rlnc_amd.Context(0)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    rng = np.random.default_rng(11)
+    k, L = 32, 1 << 16
+    data = rng.integers(0, 256, k * L, dtype=np.uint8)
+    enc = Encoder.without_padding(data, k, ctx)
+    n = 64
+    ca, cb = (rng.integers(0, 256, (n, k), dtype=np.uint8) for _ in range(2))
+    with torch.cuda.stream(sa):
+        ca_dev = torch.from_numpy(ca).cuda()
+        out_a = torch.zeros((n, k + L), dtype=torch.uint8, device="cuda")
+        ctx.use_torch_stream()
+        keep = _long_batch(torch, ctx, 60)
+        enc.code_batch_device(ca_dev.data_ptr(), n, out_a.data_ptr())
+    with torch.cuda.stream(sb):
+        cb_dev = torch.from_numpy(cb).cuda()
+        out_b = torch.zeros((n, k + L), dtype=torch.uint8, device="cuda")
+        ctx.use_torch_stream()
+        enc.code_batch_device(cb_dev.data_ptr(), n, out_b.data_ptr())
+        del enc
+        other = rng.integers(0, 256, k * L, dtype=np.uint8)
+        enc2 = Encoder.without_padding(other, k, ctx)  # same size: the cached block
+    torch.cuda.synchronize()
+    src = data.reshape(k, L)
+    assert np.array_equal(out_a.cpu().numpy(), orc.encode(src, ca))
+    assert np.array_equal(out_b.cpu().numpy(), orc.encode(src, cb))
+    del enc2, keep
