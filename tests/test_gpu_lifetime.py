@@ -105,9 +105,11 @@ def test_dropped_encoder_block_reused_only_after_its_launches():
 
 
 def test_block_reused_only_after_uses_on_two_streams():
-    """An encoder used on stream A (behind ~40 ms of other work) and then on stream B (nothing ahead): dropping it
-    must wait for A's launch too, not only for the latest use on B, before the block cache hands the block to a new
-    encoder whose upload overwrites the source."""
+    """An encoder used on stream A (behind a GPU spin of tens of ms that touches none of the context's workspaces) and
+    then on stream B (nothing ahead): dropping it must wait for A's launch too, not only for the latest use on B,
+    before the block cache hands the block to a new encoder whose upload overwrites the source.  (The context's
+    workspaces are stream-ordered: the two launches never overlap here, A's runs after B's.)  Where B shares a
+    hardware queue with A, B's launch itself runs after A's and the case passes either way.)"""
     import torch
 
     import rlnc_amd
@@ -117,29 +119,37 @@ def test_block_reused_only_after_uses_on_two_streams():
     build()
     orc = Oracle()
     ctx = rlnc_amd.Context(0)
-    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    # B at high priority: a hardware queue of its own, so its launch runs while A still spins (two streams of one
+    # priority may share a queue and serialise, which would hide the case)
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream(priority=-1)
     rng = np.random.default_rng(11)
     k, L = 32, 1 << 16
     data = rng.integers(0, 256, k * L, dtype=np.uint8)
     enc = Encoder.without_padding(data, k, ctx)
     n = 64
     ca, cb = (rng.integers(0, 256, (n, k), dtype=np.uint8) for _ in range(2))
+    ca_dev, cb_dev = torch.from_numpy(ca).cuda(), torch.from_numpy(cb).cuda()
+    out_a = torch.zeros((n, k + L), dtype=torch.uint8, device="cuda")
+    out_b = torch.zeros((n, k + L), dtype=torch.uint8, device="cuda")
+    # one launch first: the context's workspaces grow to this shape now (a growth frees the old buffer, and hipFree
+    # waits for the whole device, which would run A's spin out before B's launch)
+    enc.code_batch_device(cb_dev.data_ptr(), n, out_b.data_ptr())
+    torch.cuda.synchronize()
+    out_b.zero_()
     with torch.cuda.stream(sa):
-        ca_dev = torch.from_numpy(ca).cuda()
-        out_a = torch.zeros((n, k + L), dtype=torch.uint8, device="cuda")
+        torch.cuda._sleep(200_000_000)
         ctx.use_torch_stream()
-        keep = _long_batch(torch, ctx, 60)
         enc.code_batch_device(ca_dev.data_ptr(), n, out_a.data_ptr())
     with torch.cuda.stream(sb):
-        cb_dev = torch.from_numpy(cb).cuda()
-        out_b = torch.zeros((n, k + L), dtype=torch.uint8, device="cuda")
         ctx.use_torch_stream()
         enc.code_batch_device(cb_dev.data_ptr(), n, out_b.data_ptr())
+        still_waiting = not sa.query()  # A's launch has not run yet when the encoder is dropped
         del enc
         other = rng.integers(0, 256, k * L, dtype=np.uint8)
         enc2 = Encoder.without_padding(other, k, ctx)  # same size: the cached block
     torch.cuda.synchronize()
     src = data.reshape(k, L)
-    assert np.array_equal(out_a.cpu().numpy(), orc.encode(src, ca))
+    assert still_waiting, "stream A's spin ended before the drop: the case was not exercised"
     assert np.array_equal(out_b.cpu().numpy(), orc.encode(src, cb))
-    del enc2, keep
+    assert np.array_equal(out_a.cpu().numpy(), orc.encode(src, ca))
+    del enc2
