@@ -27,7 +27,9 @@
  *     context's own workspaces: one caller thread per context at a time (one context per stream).
  *   - Lifetime.  Objects hold a reference on the context that created them: rlnc_context_destroy drops the
  *     creator's reference and the context is freed when its last object is freed, so an object may outlive
- *     the thread (and thread-local context) that created it.
+ *     the thread (and thread-local context) that created it.  Freeing an object waits only for its own
+ *     stream-ordered uses (its _batch_device / _device launches, on whichever streams the context had then),
+ *     not for other work queued on the context's stream; its device memory is reused only after them.
  *   - HIP graphs.  Once a batch call on a context has been captured into a HIP graph, the graph holds that
  *     context's workspace addresses: they are frozen, and a later call that would need a larger workspace
  *     fails with RLNC_ERR_INVALID_ARGUMENT instead of moving them (run the largest shape eagerly before
@@ -286,9 +288,9 @@ int rlnc_encoder_new_device(rlnc_context *ctx, const uint8_t *data_dev, size_t d
                             rlnc_encoder **out);
 /* Ragged batches: every object with its own shape and buffers (device pointers; strides 0 = dense), as a sender or
  * receiver holding pieces of many objects has them.  Each kernel stage is one launch over a device-side descriptor
- * table, whatever the number of objects and shapes (the matmul stage: <= 4 launches -- block addresses, the
- * bit-sliced program for <= 32 and > 32 output rows, the perm kernel for < 4 KiB tails -- and for misaligned
- * operands on a device without unaligned vector access, rlnc_device_unaligned_vector_access).
+ * table, whatever the number of objects and shapes (the matmul stage: <= 6 launches -- block addresses, the
+ * bit-sliced program for <= 8, <= 16, <= 32 and > 32 output rows, the perm kernel for < 4 KiB tails -- and for
+ * misaligned operands on a device without unaligned vector access, rlnc_device_unaligned_vector_access).
  * Asynchronous on the context stream.  Error checks run over all descriptors before anything is launched.
  * rlnc_encode_ragged: n coded pieces coeffs ‖ data per object (encoder.rs:241-250 × n). */
 typedef struct rlnc_object_desc {
