@@ -108,6 +108,8 @@ struct CallWs {
     PinBuf pc_coef, pc_out, pc_flag;
     DevBuf pc_count;
     size_t pc_count_words = 0;  // zeroed words of pc_count
+    DevBuf pc_part, pc_pcount;  // split products (piece.hpp): partial slabs and per-block counters
+    size_t pc_pcount_words = 0;  // zeroed words of pc_pcount
     uint32_t epoch = 0;
     CallWs() { pc_coef.flags = pc_out.flags = pc_flag.flags = hipHostMallocCoherent; }
     ~CallWs() {

@@ -218,6 +218,18 @@ int piece_chunk_blocks() {
 // out rows r < n_out: dst[r·dst_row + 0 : width) = XOR_j coef[r·coef_row + j] · in[j·in_row + 0 : width), j < n_in.
 // coef: host memory; one row of at most kPieceInline bytes travels in the kernel arguments, more are read by the kernel
 // from ws->pc_coef (coef may already point there).  Synchronous: returns once dst holds every row.
+// workgroups per (row, column block) of the call-latency kernel: rlnc::piece_split, or RLNC_PIECE_SPLIT (A/B knob,
+// read once: 1 = never split, n = n workgroups whenever n_in > 64; 0 / unset = rlnc::piece_split)
+int piece_split_for(int n_in, int64_t blocks) {
+    static const int forced = [] {
+        const char *e = getenv("RLNC_PIECE_SPLIT");
+        return e ? std::max(0, atoi(e)) : 0;
+    }();
+    if (forced == 1) return 1;
+    if (forced > 1) return n_in > 64 ? std::min(forced, 32) : 1;
+    return rlnc::piece_split(n_in, blocks);
+}
+
 int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t width, const uint8_t *coef,
                size_t coef_row, size_t n_out, uint8_t *dst, size_t dst_row) {
     const uint64_t t0 = g_piece_trace.on ? now_ns() : 0;
@@ -246,13 +258,26 @@ int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t
         HIP_TRY(hipMemsetAsync(ws->pc_count.p, 0, chunks * 4, ws->stream));
         ws->pc_count_words = chunks;
     }
+    const int64_t gx = (p.width + rlnc::kPieceCols - 1) / rlnc::kPieceCols;
+    p.split = piece_split_for(p.n_in, gx * int64_t(n_out));
+    if (p.split > 1) {
+        const size_t blocks = size_t(gx) * n_out;
+        if (int st = ws->pc_part.ensure(blocks * size_t(p.split) * 64 * 16)) return st;
+        if (blocks > ws->pc_pcount_words) {
+            if (int st = ws->pc_pcount.ensure(blocks * 4)) return st;
+            HIP_TRY(hipMemsetAsync(ws->pc_pcount.p, 0, blocks * 4, ws->stream));
+            ws->pc_pcount_words = blocks;
+        }
+        p.part = ws->pc_part.as<uint4>();
+        p.pcount = ws->pc_pcount.as<uint32_t>();
+    }
     p.out = ws->pc_out.as<uint8_t>();
     p.count = ws->pc_count.as<uint32_t>();
     p.flag = ws->pc_flag.as<uint32_t>();
     if (++ws->epoch == 0) ws->epoch = 1;
     p.epoch = ws->epoch;
     const uint64_t t1 = g_piece_trace.on ? now_ns() : 0;
-    HIP_TRY(rlnc::launch_piece(p, piece_waves_for(p.n_in), ws->stream));
+    HIP_TRY(rlnc::launch_piece(p, piece_waves_for((p.n_in + p.split - 1) / p.split), ws->stream));
     const uint64_t t2 = g_piece_trace.on ? now_ns() : 0;
     uint64_t t3 = 0;
     const size_t chunk_bytes = size_t(p.chunk_blocks) * rlnc::kPieceCols;
@@ -262,6 +287,7 @@ int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t
             // a failed launch may leave counters part-way: wait for the stream and re-arm them
             (void)hipStreamSynchronize(ws->stream);
             ws->pc_count_words = 0;
+            ws->pc_pcount_words = 0;
             return st;
         }
         if (c == 0 && g_piece_trace.on) t3 = now_ns();

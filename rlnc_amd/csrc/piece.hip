@@ -20,6 +20,8 @@
 //     (1.7-6.5 us), per workgroup -- 1 MiB rows took 4x longer with one (profiles/r04_object_api_bench.txt).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "gf256.hpp"
 #include "kernels_common.hpp"
 #include "piece.hpp"
@@ -47,14 +49,17 @@ __device__ __forceinline__ void mac16(uint32_t (&acc)[4], const uint4 x, uint32_
     }
 }
 
-// grid (ceil(width / kPieceCols), n_out); block 64·W threads (W = 1, 2, 4, 8 or 16 waves)
+// grid (ceil(width / kPieceCols), n_out, split); block 64·W threads (W = 1, 2, 4, 8 or 16 waves)
 __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PieceParams p) {
     __shared__ uint4 red[kPieceMaxWaves - 1][64];
     const int W = int(blockDim.x) >> 6;
     const int w = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
     const int row = int(blockIdx.y);
-    const int R = (p.n_in + W - 1) / W;
-    const int r0 = min(p.n_in, w * R), r1 = min(p.n_in, r0 + R);
+    // this workgroup's sources: part z of `split` (z = blockIdx.z), then wave w's share of them
+    const int RS = (p.n_in + p.split - 1) / p.split;
+    const int s0 = min(p.n_in, int(blockIdx.z) * RS), s1 = min(p.n_in, s0 + RS);
+    const int R = (s1 - s0 + W - 1) / W;
+    const int r0 = min(s1, s0 + w * R), r1 = min(s1, r0 + R);
     const int64_t col = int64_t(blockIdx.x) * kPieceCols + lane * 16;
     const bool live = col < p.width;
     // source rows are padded to 16 bytes (in_row >= round16(width)): the last slot loads whole.  Every load is
@@ -95,6 +100,32 @@ __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PiecePara
                 acc[3] ^= o.w;
             }
     }
+    if (p.split > 1) {
+        // every wave but wave 0 is done; wave 0 publishes this workgroup's partial and counts it (the hand-off form of
+        // MI355X_MICROARCH.md §inter-workgroup visibility: write-through stores drained by s_waitcnt vmcnt(0), one
+        // lane's agent-scope add, the last adder -- told by the value its add returned -- loads the others' bytes with
+        // write-through loads), and only the last of the block's `split` workgroups goes on to the output
+        if (w > 0) return;
+        const int64_t blk = int64_t(row) * gridDim.x + blockIdx.x;
+        const __amdgpu_buffer_rsrc_t prs =
+            __builtin_amdgcn_make_buffer_rsrc(p.part + blk * p.split * 64, 0, 0x7FFFFFFF, 0x00020000);
+        const u32x4 mine = {acc[0], acc[1], acc[2], acc[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(mine, prs, int((blockIdx.z * 64 + lane) * 16), 0, kSysWriteThrough);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t prev = 0;
+        if (lane == 0) prev = __hip_atomic_fetch_add(p.pcount + blk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        prev = uint32_t(__shfl(int(prev), 0));
+        if (prev != uint32_t(p.split - 1)) return;
+        if (lane == 0) __hip_atomic_store(p.pcount + blk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int z = 0; z < p.split; ++z) {
+            if (z == int(blockIdx.z)) continue;
+            const u32x4 o = __builtin_amdgcn_raw_buffer_load_b128(prs, (z * 64 + lane) * 16, 0, kSysWriteThrough);
+            acc[0] ^= o.x;
+            acc[1] ^= o.y;
+            acc[2] ^= o.z;
+            acc[3] ^= o.w;
+        }
+    }
     // the output row is padded to 16 bytes too (out_row >= round16(width)): the last slot stores whole.  Stores are
     // write-through to system scope (sc0 sc1), so no release fence (an L2 write-back per workgroup) is needed before
     // the workgroup is counted: every storing wave drains its stores, the workgroup meets at a barrier, one lane adds
@@ -108,7 +139,7 @@ __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PiecePara
     }
     if (p.flag == nullptr) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (p.split == 1) __syncthreads();  // (split > 1: wave 0 is the only one left)
     if (p.chunk_blocks == 1) {  // a flag per workgroup: no counter
         if (threadIdx.x == 0)
             __hip_atomic_store(p.flag + int64_t(row) * gridDim.x + blockIdx.x, p.epoch, __ATOMIC_RELAXED,
@@ -135,6 +166,17 @@ __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PiecePara
 // measured 1-1.5 us slower at 16-64 sources: more waves to launch and to reduce)
 int piece_waves(int n_in) { return n_in <= 32 ? 4 : n_in <= 128 ? 8 : kPieceMaxWaves; }
 
+// More than 128 sources over few column blocks (the 1 MB encode at k = 256: 5 blocks): about 64 sources per workgroup,
+// at most 32 workgroups per block.  The hand-off (partial stores drained, the counter, the last workgroup's loads)
+// costs ~2-3 us, which only pays where a workgroup would otherwise walk 16 sources a wave: 1 MB encode at k = 256
+// kernel 12.1 -> 8.9 us (call 17.0-17.3 -> 14.2-15.1), while at 128 sources (k = 128 encode, k = 256 recode) the
+// split measured no faster or slower (profiles/r04_split_ab.txt).  Wide rows keep one workgroup per block (enough
+// workgroups already; the partials would be extra traffic).
+int piece_split(int n_in, int64_t blocks) {
+    if (n_in <= 128 || blocks >= 64) return 1;
+    return std::min(32, (n_in + 63) / 64);
+}
+
 int piece_chunks(const PieceParams &p) {
     const int64_t gx = (p.width + kPieceCols - 1) / kPieceCols;
     return int((gx + p.chunk_blocks - 1) / p.chunk_blocks) * p.n_out;
@@ -146,13 +188,15 @@ hipError_t launch_piece(const PieceParams &p, int waves, hipStream_t s) {
         return hipErrorInvalidValue;
     if (p.coef == nullptr && (p.n_out != 1 || p.n_in > kPieceInline)) return hipErrorInvalidValue;
     if (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16) return hipErrorInvalidValue;
+    if (p.split < 1 || p.split > 64 || (p.split > 1 && (p.part == nullptr || p.pcount == nullptr))) return hipErrorInvalidValue;
     if ((reinterpret_cast<uintptr_t>(p.in) | reinterpret_cast<uintptr_t>(p.out) | uintptr_t(p.in_row) |
          uintptr_t(p.out_row)) & 15)
         return hipErrorInvalidValue;
     const int64_t padded = (p.width + 15) & ~int64_t(15);
     if (padded > 0x7FFFFFF0LL) return hipErrorInvalidValue;  // 32-bit buffer offsets within a row
     if (p.in_row < padded || (p.n_out > 1 && p.out_row < padded)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(gf_piece_kernel, dim3(unsigned(gx), unsigned(p.n_out)), dim3(64 * waves), 0, s, p);
+    hipLaunchKernelGGL(gf_piece_kernel, dim3(unsigned(gx), unsigned(p.n_out), unsigned(p.split)), dim3(64 * waves), 0, s,
+                       p);
     return hipGetLastError();
 }
 

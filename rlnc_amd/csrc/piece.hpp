@@ -31,12 +31,20 @@ struct PieceParams {
     uint32_t *flag;
     uint32_t epoch;
     int chunk_blocks;
+    // split > 1: the sources are also split over `split` workgroups per (row, column block) (grid z): each stores its
+    // partial 1 KiB (part: split · n_out · gx slabs of 64 uint4, device memory, write-through) and adds to the block's
+    // counter (pcount: n_out · gx device words, zero before the first launch); the last to add XORs the others' partials
+    // in, re-arms the counter and goes on as a split = 1 workgroup (output row slot, chunk counting)
+    int split;
+    uint4 *part;
+    uint32_t *pcount;
     // coef == nullptr: the coefficients are these bytes (n_out == 1): read from the kernel-argument segment in device
     // memory instead of across PCIe from pinned host memory (a round trip at the head of every workgroup)
     uint8_t coef_inline[kPieceInline];
 };
 
 int piece_waves(int n_in);  // waves per workgroup for n_in sources
+int piece_split(int n_in, int64_t blocks);  // workgroups per (row, column block) for n_in sources over `blocks` of them
 int piece_chunks(const PieceParams &p);
 hipError_t launch_piece(const PieceParams &p, int waves, hipStream_t s);
 
