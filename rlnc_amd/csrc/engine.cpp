@@ -183,14 +183,25 @@ struct PieceTrace {
         const char *e = getenv("RLNC_PIECE_TRACE");
         return e && atoi(e) != 0;
     }();
-    std::atomic<uint64_t> calls{0}, ns_pre{0}, ns_launch{0}, ns_first{0}, ns_rest{0};
+    std::mutex mu;
+    std::vector<float> pre, launch, first, rest;  // per call, us
+    void add(uint64_t a, uint64_t b, uint64_t c, uint64_t d) {
+        std::lock_guard<std::mutex> lock(mu);
+        pre.push_back(a / 1e3f);
+        launch.push_back(b / 1e3f);
+        first.push_back(c / 1e3f);
+        rest.push_back(d / 1e3f);
+    }
+    static float med(std::vector<float> v) {
+        if (v.empty()) return 0.f;
+        std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+        return v[v.size() / 2];
+    }
     ~PieceTrace() {
-        const uint64_t n = calls.load();
-        if (on && n)
-            std::fprintf(stderr, "{\"piece_trace\": {\"calls\": %llu, \"pre_us\": %.2f, \"launch_us\": %.2f, "
-                                 "\"to_first_flag_us\": %.2f, \"copies_and_rest_us\": %.2f}}\n",
-                         (unsigned long long)n, ns_pre / 1e3 / n, ns_launch / 1e3 / n, ns_first / 1e3 / n,
-                         ns_rest / 1e3 / n);
+        if (on && !pre.empty())
+            std::fprintf(stderr, "{\"piece_trace\": {\"calls\": %zu, \"median_pre_us\": %.2f, \"median_launch_us\": %.2f, "
+                                 "\"median_to_first_flag_us\": %.2f, \"median_copies_and_rest_us\": %.2f}}\n",
+                         pre.size(), med(pre), med(launch), med(first), med(rest));
     }
 };
 PieceTrace g_piece_trace;
@@ -294,14 +305,7 @@ int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t
         const size_t r = c / cpr, c0 = (c % cpr) * chunk_bytes, c1 = std::min(width, c0 + chunk_bytes);
         std::memcpy(dst + r * dst_row + c0, p.out + r * size_t(p.out_row) + c0, c1 - c0);
     }
-    if (g_piece_trace.on) {
-        const uint64_t t4 = now_ns();
-        g_piece_trace.calls += 1;
-        g_piece_trace.ns_pre += t1 - t0;
-        g_piece_trace.ns_launch += t2 - t1;
-        g_piece_trace.ns_first += t3 - t2;
-        g_piece_trace.ns_rest += t4 - t3;
-    }
+    if (g_piece_trace.on) g_piece_trace.add(t1 - t0, t2 - t1, t3 - t2, now_ns() - t3);
     return RLNC_OK;
 }
 

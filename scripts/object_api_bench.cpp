@@ -82,6 +82,8 @@ int main(int argc, char **argv) {
         const Cfg c = kArgs[a];
         if (quick && c.bytes > (1u << 24)) continue;
         if (std::getenv("OBJ_BENCH_SMALL") && c.bytes > (1u << 20)) continue;  // the 1 MB rows only
+        if (const char *kk = std::getenv("OBJ_BENCH_K"))  // one k only (e.g. with RLNC_PIECE_TRACE=1)
+            if (size_t(std::atoi(kk)) != c.k) continue;
         std::vector<uint8_t> data(c.bytes);
         rng.fill_bytes(data.data(), data.size());
         Encoder enc = Encoder::create(data, c.k).unwrap();
