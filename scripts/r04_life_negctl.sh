@@ -1,5 +1,8 @@
 # negative control of tests/test_gpu_lifetime.py::test_block_reused_only_after_uses_on_two_streams: the library built
-# without ObjUse's cross-stream wait (build/negctl) must fail it; the shipped library passes it
+# without ObjUse's cross-stream wait (build/negctl) must fail it; the shipped library passes it.  Build the control
+# first (on the CPU):
+#   mkdir -p build/negctl && sed 's/        if (used \&\& s != last) HIP_TRY(hipStreamWaitEvent(s, ev, 0));/        \/\/ negative control/' \
+#       rlnc_amd/csrc/context.hpp > build/negctl/context.hpp && scripts/diag_build.sh build/negctl context.hpp=build/negctl/context.hpp
 set -o pipefail
 mkdir -p gpurun_out
 T="tests/test_gpu_lifetime.py::test_block_reused_only_after_uses_on_two_streams"
