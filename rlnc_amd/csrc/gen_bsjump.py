@@ -907,6 +907,10 @@ def main():
     ap.add_argument("--slots1", type=int, default=3, help="ring slots of the 1-wave program (3 = the 2-row form)")
     ap.add_argument("--slots2", type=int, default=3, help="ring slots of the 2-wave program (3 = the 2-row form)")
     ap.add_argument("--store-hint", default="", help="cache-policy modifiers of the tile stores, e.g. 'nt' (A/B)")
+    # the 1- and 2-wave programs (<= 16 output rows: many small objects, HBM-bound) store non-temporally: configs[0]'s
+    # 4,096 x 16 x 4 KiB encode 0.149 -> 0.142 ms, decode 0.179 -> 0.169 (profiles/r04_hint_cfg0_ab.txt); the 4- and
+    # 8-wave programs keep plain stores (no gain on the VALU-bound bench, profiles/r02_cache_hint_ab.txt)
+    ap.add_argument("--store-hint-small", default="nt", help="tile-store modifiers of the 1- and 2-wave programs")
     args = ap.parse_args()
     HINTS["load"], HINTS["store"] = args.load_hint, args.store_hint
     global PRIO_AT
@@ -935,7 +939,11 @@ def main():
         for w in (1, 2, 4):
             WAVES, WG_ROWS = w, NT * w
             STREAM_J_BYTES = WG_ROWS * 4
+            saved = HINTS["store"]
+            if w <= 2 and not HINTS["store"]:
+                HINTS["store"] = args.store_hint_small
             body_txt = "\\n\\t".join(hinted(program({1: args.slots1, 2: args.slots2}.get(w, SLOTS))))
+            HINTS["store"] = saved
             f.write(f'#define RLNC_BSJ_ASM_W{w} "{body_txt}"\n')
         WAVES, WG_ROWS = 4, NT * 4
         STREAM_J_BYTES = WG_ROWS * 8  # 64-bit block addresses

@@ -14,5 +14,5 @@ build() {  # name load-hint store-hint
 build stnt "" "nt" &
 build ldnt "nt" "" &
 build bothnt "nt" "nt" &
-build stsc1 "" "sc1" &
+[ -n "${SKIP_SC1:-}" ] || build stsc1 "" "sc1" &
 wait
