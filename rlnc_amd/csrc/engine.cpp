@@ -1116,7 +1116,8 @@ int rlnc_recode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t k, size_t
 // The elimination alone: reads only the k coefficient bytes of each piece; writes T [obj][k][m], the per-piece
 // statuses and the ranks.
 static int decode_eliminate_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
-                                 size_t m, size_t nobj, uint8_t *T, int32_t *pstat_dev, int32_t *rank_dev) {
+                                 size_t m, size_t nobj, uint8_t *T, int32_t *pstat_dev, int32_t *rank_dev,
+                                 uint32_t *bsj = nullptr, int bsj_rows = 0, bool *bsj_written = nullptr) {
     const size_t full = k + L;
     rlnc::RrefParams rp{};
     rp.pieces = pieces;
@@ -1132,14 +1133,17 @@ static int decode_eliminate_impl(rlnc_context *ctx, const uint8_t *pieces, size_
     rp.lds_only = ctx->decode_path == 3 ? 1 : ctx->decode_path == 4 ? 2 : ctx->decode_path == 5 ? 3 : ctx->decode_path == 6 ? 4 : 0;
     if (ctx->decode_path == 5 && !rlnc::rref_block_eligible(int(k), int(m)))  // no silent fallback to another kernel
         return set_error(RLNC_ERR_INVALID_ARGUMENT, "decode path 5 (blocked run) needs k + m <= 256 (k=%zu, m=%zu)", k, m);
-    HIP_TRY(rlnc::launch_rref_batch(rp, ctx->stream));
+    rp.bsj_stream = bsj;
+    rp.bsj_block_bytes = rlnc::bsj_block_bytes_public();
+    rp.bsj_tile_rows = bsj_rows;
+    HIP_TRY(rlnc::launch_rref_batch(rp, ctx->stream, bsj_written));
     return RLNC_OK;
 }
 
 // The data side: decoded = T × received data (one matmul), then the marker scan (decoder.rs:136-177).
 static int decode_apply_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
                              size_t m, size_t nobj, const uint8_t *T, const int32_t *rank_dev, uint8_t *decoded,
-                             int32_t *ostat_dev, int64_t *len_dev) {
+                             int32_t *ostat_dev, int64_t *len_dev, const void *bsj = nullptr, int bsj_rows = 0) {
     const size_t full = k + L;
     int st;
     rlnc::MatmulParams p{};
@@ -1156,6 +1160,8 @@ static int decode_apply_impl(rlnc_context *ctx, const uint8_t *pieces, size_t ob
     p.n_in = int(m);
     p.width = int64_t(L);
     p.n_obj = int(nobj);
+    p.bsj_stream = bsj;
+    p.bsj_stream_rows = bsj_rows;
     if ((st = ctx->matmul(p))) return st;
     HIP_TRY(rlnc::launch_final_data_len_ranked(decoded, int64_t(k * L), int64_t(k * L), int(nobj), int(k), rank_dev,
                                                ostat_dev, len_dev, ctx->stream));
@@ -1171,8 +1177,20 @@ static int decode_batch_device_impl(rlnc_context *ctx, const uint8_t *pieces, si
     // (Eliminating the later objects on a second stream beside the first objects' T x data product measured slower:
     // 8.3-8.6 ms against 7.99 for configs[4]'s 512 objects -- the concurrent elimination slows the product more
     // than it hides; profiles/r02_decode_pipeline_ab.txt.)
-    if ((st = decode_eliminate_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, pstat_dev, rank_dev))) return st;
-    return decode_apply_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, rank_dev, decoded, ostat_dev, len_dev);
+    // small objects (the one-wave elimination kernel, products in the 1- or 2-wave bit-sliced program): the elimination
+    // also writes the product's block-offset stream, so the product needs no offset launch (configs[0] shape: -6 us)
+    const int bsj_rows = rlnc::bsj_unshared_tile_rows(int(k));
+    uint32_t *bsj = nullptr;
+    if (bsj_rows > 0) {
+        if ((st = ctx->grow(ctx->ws_bsj, nobj * m * size_t(bsj_rows) * 4 + 512))) return st;
+        bsj = ctx->ws_bsj.as<uint32_t>();
+    }
+    bool written = false;
+    if ((st = decode_eliminate_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, pstat_dev, rank_dev, bsj, bsj_rows,
+                                    &written)))
+        return st;
+    return decode_apply_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, rank_dev, decoded, ostat_dev, len_dev,
+                             written ? bsj : nullptr, written ? bsj_rows : 0);
 }
 
 // Host path (matrices too large for LDS): exact elimination on host threads (elimination.hpp).

@@ -651,6 +651,10 @@ hipError_t bsj_prepare(const MatmulParams &p, hipStream_t s, void *scratch, size
     b.col_blocks = int(b.full / kBsjColBlock);
     b.total = int64_t(p.n_obj) * b.row_tiles * b.col_blocks;
     if (b.total > 0x7FFFFFFFLL || p.n_obj > 65535) return hipErrorInvalidValue;
+    if (!abs && p.bsj_stream != nullptr && p.bsj_stream_rows == tile_rows) {  // written by the elimination already
+        b.stream = const_cast<void *>(p.bsj_stream);
+        return hipSuccess;
+    }
     b.stream = scratch;
     const int64_t per_obj = int64_t(b.row_tiles) * p.n_in * tile_rows;
     if ((per_obj + 255) / 256 > 0x7FFFFFFFLL) return hipErrorInvalidValue;
@@ -1323,6 +1327,7 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
             for (int64_t c0 = 0; c0 < p.width; c0 += r.cw) {
                 const int64_t w = std::min(r.cw, p.width - c0);
                 MatmulParams q = p;
+                q.bsj_stream = nullptr;  // laid out for the whole batch
                 q.n_obj = c;
                 q.width = w;
                 q.in = p.in + int64_t(o0) * p.in_obj + c0;
@@ -1403,6 +1408,8 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
 }
 
 bool bsj_eligible_public(const MatmulParams &p) { return bsj_eligible(p, matmul_aligned(p)); }
+uint32_t bsj_block_bytes_public() { return uint32_t(RLNC_BSJ_BLOCK_BYTES); }
+int bsj_unshared_tile_rows(int n_out) { return bsj_waves(n_out) <= 2 ? kBsjWaveRows * bsj_waves(n_out) : 0; }
 size_t bsj_scratch_bytes_public(const MatmulParams &p, bool wide) { return bsj_scratch_bytes(p, wide); }
 
 // The A/B build (make ab) links kernels_ab.hip, whose definitions replace these

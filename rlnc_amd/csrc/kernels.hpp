@@ -27,6 +27,11 @@ struct MatmulParams {
     int64_t width;
     int n_obj;
     int col_run = 0;  // column blocks per workgroup of the column-run program (variant 9): 0 = chosen per launch
+    // optional: the block-offset stream of this product already written (by the small-object elimination, rref.hip):
+    // 4-byte offsets laid out as bsj_offset_kernel<false> lays them out for tiles of bsj_stream_rows rows; used when
+    // the product takes the 1- or 2-wave bit-sliced program with exactly those tiles, else ignored
+    const void *bsj_stream = nullptr;
+    int bsj_stream_rows = 0;
 };
 
 enum class MatmulVariant : int {
@@ -146,6 +151,12 @@ struct RrefParams {
     // (the general kernel over all pieces) skips the objects pass 1 full-ranked (skip_full) and redoes the others
     int m_stride = 0;   // 0 = m
     int skip_full = 0;
+    // optional (the small-object kernel only): also write T as the 1- / 2-wave bit-sliced program's block-offset
+    // stream -- bsj_stream[o][j][i] = T[i][j] · bsj_block_bytes for i < bsj_tile_rows (0 past k) -- so the T × data
+    // product needs no offset launch (MatmulParams::bsj_stream); launch_rref_batch reports whether it did
+    uint32_t *bsj_stream = nullptr;
+    uint32_t bsj_block_bytes = 0;
+    int bsj_tile_rows = 0;
 };
 // One object of a ragged elimination launch (rlnc_decode_ragged): T is k x m row-major, status m entries.
 struct RrefObj {
@@ -167,7 +178,10 @@ constexpr size_t kRrefMaxLds = 160 * 1024;
 size_t rref_lds_bytes(int k, int m);
 // the blocked clean-run kernel (decode path 5, and what 0 / 2 pick) applies: a row fits one wave (k + m <= 256)
 bool rref_block_eligible(int k, int m);
-hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s);
+hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s, bool *bsj_written = nullptr);
+// block bytes and tile rows of the unshared bit-sliced programs (for RrefParams::bsj_*): tile rows 0 = not one of them
+uint32_t bsj_block_bytes_public();
+int bsj_unshared_tile_rows(int n_out);
 
 // final_len with the decoder's rank: objects with rank < k report NotAllPiecesReceivedYet
 hipError_t launch_final_data_len_ranked(const uint8_t *data, int64_t obj_stride, int64_t len, int n_obj, int k,

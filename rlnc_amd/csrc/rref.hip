@@ -80,12 +80,13 @@ hipError_t launch_rref_ragged(const RrefObj *objs, int n, bool block, size_t lds
     return hipGetLastError();
 }
 
-static hipError_t launch_rref_one(const RrefParams &p, hipStream_t s);
+static hipError_t launch_rref_one(const RrefParams &p, hipStream_t s, bool *bsj_written);
 
 // k + m > 256 with k <= 128: the blocked run over the first 256 - k pieces (>= k), then the general kernel over all m
 // pieces for the objects that did not reach rank k within them (with dense coefficients: none).  Same outputs as the
 // general kernel alone (RrefParams::m_stride); 32 objects of k = 128, m = 130: 4.0 ms in the one-wave LDS kernel.
-hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
+hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s, bool *bsj_written) {
+    if (bsj_written) *bsj_written = false;
     if (p.n_obj <= 0) return hipSuccess;
     if (p.lds_only == 0 && p.objs == nullptr && p.m_stride == 0 && !p.skip_full && p.k <= 128 &&
         rref_row_dwords(p.k, p.m) > 64 && rref_lds_bytes(p.k, p.m) <= kRrefMaxLds &&
@@ -93,16 +94,18 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s) {
         RrefParams a = p;
         a.m = 256 - p.k;
         a.m_stride = p.m;
-        hipError_t e = launch_rref_one(a, s);
+        a.bsj_stream = nullptr;
+        hipError_t e = launch_rref_one(a, s, nullptr);
         if (e != hipSuccess) return e;
         RrefParams b = p;
         b.skip_full = 1;
-        return launch_rref_one(b, s);
+        b.bsj_stream = nullptr;
+        return launch_rref_one(b, s, nullptr);
     }
-    return launch_rref_one(p, s);
+    return launch_rref_one(p, s, bsj_written);
 }
 
-static hipError_t launch_rref_one(const RrefParams &p, hipStream_t s) {
+static hipError_t launch_rref_one(const RrefParams &p, hipStream_t s, bool *bsj_written) {
     hipError_t ab = hipSuccess;
     if (launch_rref_ab(p, s, &ab)) return ab;  // the A/B build's paths (rref_ab.hip); false in the shipped library
     // many small objects (k <= 16, >= 2048 of them: 8 per CU and more): the one-wave register kernel (path 4's)
@@ -147,7 +150,9 @@ static hipError_t launch_rref_one(const RrefParams &p, hipStream_t s) {
         int nw = g8 ? kSmallNW : 1;
         const size_t lds_small = size_t(kTabEntries) * kTabDw * 4 + nw * rref_small_wave_bytes(p.k, p.m);
         hipLaunchKernelGGL(kern, dim3((p.n_obj + nw - 1) / nw), dim3(64 * nw), lds_small, s, p);
-        return hipGetLastError();
+        const hipError_t e = hipGetLastError();
+        if (e == hipSuccess && bsj_written) *bsj_written = p.bsj_stream != nullptr && p.bsj_tile_rows > 0;
+        return e;
     }
     size_t lds = rref_lds_bytes(p.k, p.m);
     if (lds > kRrefMaxLds) return hipErrorInvalidValue;

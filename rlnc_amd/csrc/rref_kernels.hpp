@@ -936,6 +936,14 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 
         const int r = e / m, s = e % m;
         T[e] = r < rows ? M.b[r * M.S + k + s] : uint8_t(0);
     }
+    if (p.bsj_stream != nullptr) {  // T again, as the product's block-offset stream ([j][i], i < tile rows)
+        const int tr = p.bsj_tile_rows;
+        uint32_t *st = p.bsj_stream + int64_t(o) * m * tr;
+        for (int e = lane; e < m * tr; e += 64) {
+            const int s = e / tr, r = e % tr;
+            st[e] = (r < rows ? uint32_t(M.b[r * M.S + k + s]) : 0u) * p.bsj_block_bytes;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------------

@@ -814,6 +814,29 @@ def test_decode_many_small_objects(ctx, k, m, sparsity, dep, nobj):
         assert S[ost[o]] == S[st], o
 
 
+@pytest.mark.parametrize("k,m,sparsity,dep,nobj,L", [(16, 16, 0.0, 0.0, 2048, 4096), (16, 24, 0.5, 0.1, 2051, 4096 + 40),
+                                                    (8, 12, 0.7, 0.1, 2049, 8192)])
+def test_decode_many_small_objects_block_products(ctx, k, m, sparsity, dep, nobj, L):
+    """As above with whole 4 KiB column blocks: the T x data product takes the 1- / 2-wave bit-sliced program, whose
+    block-offset stream the small-object elimination writes itself (engine.cpp decode_batch_device_impl, RrefParams::
+    bsj_stream) -- rank-deficient and dependent objects included, a ragged tail after the blocks in one case."""
+    from rlnc_amd import batch
+
+    rng = np.random.default_rng(4096 + k * 5 + m)
+    seqs = _sequences(rng, nobj, k, m, L, sparsity, dep)
+    decoded = dev(np.zeros((nobj, k, L), np.uint8))
+    pst, ost, dl = batch.decode_batch(dev(seqs), k, decoded, ctx)
+    got = host(decoded)
+    for o in range(nobj):
+        od = OracleDecoder(L, k)
+        want = [S[od.decode(p)] for p in seqs[o]]
+        assert [S[x] for x in pst[o]] == want, o
+        pay = od.padded_payload()
+        assert np.array_equal(got[o, : pay.shape[0]], pay), o
+        st, _ = od.get_decoded_data()
+        assert S[ost[o]] == S[st], o
+
+
 @pytest.mark.parametrize("path", [0, 2])
 def test_decode_two_pass_beyond_one_wave_row(ctx, path):
     """k + m > 256 with k <= 128: the blocked run over the first 256 - k pieces, the general kernel only for objects
