@@ -77,13 +77,33 @@ def test_many_calls_one_workspace(ctx, orc):
             assert np.array_equal(out, orc.code_with_coding_vector(src, cv)[1]), i
 
 
-def test_concurrent_calls_one_encoder(ctx, orc):
+def test_many_split_calls_one_workspace(ctx, orc):
+    """Products split across workgroups (more than 128 sources over few column blocks, piece.hip piece_split): 200
+    calls in a row on one leased workspace alternating 5 blocks x 4 workgroups and 20 blocks x 5, so each block's
+    counter must be re-armed by its last workgroup, and the partial slabs of the other shape are never read."""
+    from rlnc_amd.full import Encoder
+
+    rng = np.random.default_rng(6)
+    shapes = [(256, 4097), (300, 20000)]
+    encs = []
+    for k, L in shapes:
+        src = _src(rng, k, L)
+        encs.append((Encoder.without_padding(src.reshape(-1), k, ctx), src, np.zeros(L, np.uint8)))
+    for i in range(200):
+        enc, src, out = encs[i % 2]
+        cv = rng.integers(0, 256, src.shape[0], dtype=np.uint8)
+        enc.code_with_coding_vector(cv, out)
+        if i % 5 == 0 or i > 190:
+            assert np.array_equal(out, orc.code_with_coding_vector(src, cv)[1]), i
+
+
+@pytest.mark.parametrize("k,L", [(64, 40000), (256, 4097)])
+def test_concurrent_calls_one_encoder(ctx, orc, k, L):
     """Encoder::code is &self on a Send + Sync type (encoder.rs:264): four threads on one encoder, each call on its
-    own leased workspace."""
+    own leased workspace (k = 256: the split product, each call with its own slabs and counters)."""
     from rlnc_amd.full import Encoder
 
     rng = np.random.default_rng(11)
-    k, L = 64, 40000
     src = _src(rng, k, L)
     enc = Encoder.without_padding(src.reshape(-1), k, ctx)
     cvs = rng.integers(0, 256, (4, 40, k), dtype=np.uint8)
