@@ -46,6 +46,7 @@ MA_PER_XOR3 = 256  # GF(2^8) multiply-adds per v_bitop3 XOR3 of the bit-sliced k
 # SIMD at 2.4 GHz -> 1.2288 T XOR3/s x 256 multiply-adds = 314.6 T GF(2^8) multiply-adds/s
 SPEC_XOR3_PER_S = 256 * 4 * 2.4e9 / 2
 SPEC_PEAK_T_MA = SPEC_XOR3_PER_S * MA_PER_XOR3 / 1e12
+HARNESS_BACKEND = "gloo"  # process-group backend at every N (Dist.init)
 CPU_SHARE = 16  # host cores per GPU on the GPU box (os.cpu_count() there shows the whole machine)
 
 WORKLOADS = {
@@ -104,29 +105,31 @@ class Dist:
         self.pg = None
         self.bar = None
 
-    def init(self, backend: str):
-        """Initialise the process group (RCCL for the multi-GPU run, gloo for the CPU harness test) -- at world size
-        1 too, on a free 127.0.0.1 port, so that every line reports the world size the group initialised with.  A
-        single rank takes gloo: its barrier and reductions then stay on the host, and RCCL's own streams do not
-        share the 4 hardware queues (GPU_MAX_HW_QUEUES) with the bench's three pipeline streams (with an RCCL group
-        at N = 1 the pipelined step measured 4-5 % slower at equal kernel times)."""
+    def init(self):
+        """Initialise the process group -- at world size 1 too, on a free 127.0.0.1 port, so that every line reports
+        the world size the group initialised with.  The backend is gloo at EVERY N: the data path has no collective
+        (objects are sharded), so the group only carries the timing barrier and the scalar results, on
+        the host.  Every rank synchronises its device right before the barrier, so a host barrier orders the ranks.
+        An RCCL group would start RCCL's own streams on the 4 hardware queues the bench's three pipeline streams use
+        (the pipelined step measured 4-5 % slower with an RCCL group at N = 1) and its barrier cost ~3.5 ms per call
+        (profiles/r03_bench_pg_ab.txt); using it only at N > 1 would make the N = 1 point of a scaling curve cheaper
+        than every other point."""
         import torch.distributed as dist
 
-        if self.world == 1:
-            backend = "gloo"
-            if "MASTER_PORT" not in os.environ:
-                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-                os.environ["MASTER_PORT"] = str(_free_port())
-                os.environ.setdefault("RANK", "0")
-                os.environ.setdefault("WORLD_SIZE", "1")
-        backend = os.environ.get("RLNC_BENCH_PG", backend)  # diagnostic override of the group's backend
+        if "MASTER_PORT" not in os.environ:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ["MASTER_PORT"] = str(_free_port())
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        backend = os.environ.get("RLNC_BENCH_PG", HARNESS_BACKEND)  # diagnostic override of the group's backend
         dist.init_process_group(backend=backend)
         self.pg = dist
-        # the timing barrier on a host (gloo) group: every rank has synchronised its device just before, so a
-        # host barrier orders the ranks; an RCCL barrier inside the timed region measured ~3.5 ms per call at
-        # N = 1 (torch's NCCL barrier is an allreduce plus a device-wide wait), i.e. 7 % of a 30-step run
+        # with the diagnostic RCCL override the barrier still runs on a host group
         self.bar = dist.new_group(backend="gloo") if backend == "nccl" else None
         return self
+
+    def backend(self):
+        return self.pg.get_backend() if self.pg else None
 
     def initialised_world(self) -> int:
         return self.pg.get_world_size() if self.pg else 0
@@ -140,10 +143,19 @@ class Dist:
             return value
         import torch
 
-        dev = "cuda" if self.pg.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([value], dtype=torch.float64, device=dev)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX if op == "max" else self.pg.ReduceOp.SUM)
+        t = torch.tensor([value], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX if op == "max" else self.pg.ReduceOp.SUM, group=self.bar)
         return float(t.item())
+
+    def allgather(self, value: float) -> list:
+        """Every rank's value, in rank order (host group)."""
+        if not self.pg:
+            return [value]
+        import torch
+
+        out = [torch.zeros(1, dtype=torch.float64) for _ in range(self.world)]
+        self.pg.all_gather(out, torch.tensor([value], dtype=torch.float64), group=self.bar)
+        return [float(t.item()) for t in out]
 
     def close(self):
         if self.pg:
@@ -390,7 +402,7 @@ def run_oracle_cpu(args, dist: Dist):
 
     from oracle.oracle import Oracle, OracleDecoder
 
-    dist.init("gloo")
+    dist.init()
     orc = Oracle()
     k, L, n, m, B = 8, 512, 12, 8, 3
     strong = args.workload == "oracle-cpu-config5"
@@ -415,10 +427,12 @@ def run_oracle_cpu(args, dist: Dist):
     elapsed = timed_loop(step, args.steps, args.warmup, dist, lambda: None)
     total = dist.allreduce(float(step_bytes(B, k, L, n) * args.steps), "sum")
     total_objs = dist.allreduce(float(B), "sum")
-    ok = dist.allreduce(float(all(np.array_equal(last[o], src[o]) for o in range(B))), "sum") == dist.world
+    ok_rank = dist.allgather(float(all(np.array_equal(last[o], src[o]) for o in range(B))))
+    ok = all(v == 1.0 for v in ok_rank)
     if dist.rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(total / elapsed / GIB, 6), "unit": "GiB/s",
                           "n_gpus": dist.world, "world_size_initialised": dist.initialised_world(),
+                          "process_group_backend": dist.backend(), "verified_per_rank": [bool(v) for v in ok_rank],
                           "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True,
                           "scaling": "strong" if strong else "weak", "elapsed_s": elapsed, "total_bytes": total,
@@ -435,7 +449,7 @@ def run_gpu(args, dist: Dist):
     import torch
 
     torch.cuda.set_device(dist.local_rank)
-    dist.init("nccl")
+    dist.init()
 
     import rlnc_amd
     from rlnc_amd import batch
@@ -462,6 +476,8 @@ def run_gpu(args, dist: Dist):
 
     def buffers(B):
         return dict(pieces=torch.empty((B, n, k + L), dtype=torch.uint8, device=dev),
+                    # the encode's code-block address stream, written ahead on the side stream (encode_batch_prepare)
+                    plan=torch.empty(batch.encode_plan_bytes(k, B, n), dtype=torch.uint8, device=dev),
                     decoded=torch.empty((B, k, L), dtype=torch.uint8, device=dev),
                     pst=torch.empty((B, m), dtype=torch.int32, device=dev),
                     ost=torch.empty(B, dtype=torch.int32, device=dev),
@@ -473,8 +489,10 @@ def run_gpu(args, dist: Dist):
     sets = [buffers(C)]
     enc_events, dec_events = [], []
     ctx_side = rlnc_amd.Context(dist.local_rank) if args.pipeline else None
+    if ctx_side is not None:
+        ctx_side.set_kernel_variant(args.variant, args.tile_rows)  # the plan is laid out for the launch's variant
     side = torch.cuda.Stream(dev) if args.pipeline else None
-    ev_start, ev_elim = torch.cuda.Event(), torch.cuda.Event()
+    ev_start, ev_elim, ev_plan = torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event()
 
     def views(S, c0, c1):
         b = c1 - c0
@@ -488,21 +506,27 @@ def run_gpu(args, dist: Dist):
         s_, co, pieces, decoded, pst, ost, dl, T, rank = views(S, c0, c1)
         received = pieces[:, :m]
         e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-        e0.record()
         if args.pipeline:
-            # side stream: the coded pieces' headers (bytes 0..k of each piece), then the elimination over
-            # them; launch stream: the data bytes k.. of the same pieces (disjoint bytes), concurrently
+            # side stream: the encode's code-block address stream, the coded pieces' headers (bytes 0..k of each
+            # piece), then the elimination over them; launch stream: the data bytes k.. of the same pieces (disjoint
+            # bytes), concurrently.  e0 is recorded once the address stream is ready, so the encode part is the
+            # product kernel alone (the launches rocprofv3 attributes to gf_matmul_bsj_kernel)
             ev_start.record()
             with torch.cuda.stream(side):
                 side.wait_event(ev_start)
+                batch.encode_batch_prepare(s_, co, pieces, S["plan"], ctx_side)
+                ev_plan.record()
                 batch.encode_batch_headers(co, pieces, ctx_side)
                 if not args.encode_only:
                     batch.decode_batch_eliminate(received, k, T, pst, rank, ctx_side)
                 ev_elim.record()
-            batch.encode_batch_data(s_, co, pieces, ctx)
+            torch.cuda.current_stream().wait_event(ev_plan)
+            e0.record()
+            batch.encode_batch_data_planned(s_, co, pieces, S["plan"], ctx)
             if args.encode_only:
                 torch.cuda.current_stream().wait_event(ev_elim)
         else:
+            e0.record()
             batch.encode_batch(s_, co, pieces, ctx)
         e1.record()
         if not args.encode_only:
@@ -533,6 +557,7 @@ def run_gpu(args, dist: Dist):
         ev_done = [torch.cuda.Event(), torch.cuda.Event()]
         ev_enc = [torch.cuda.Event(), torch.cuda.Event()]
         ev_el = [torch.cuda.Event(), torch.cuda.Event()]
+        ev_pl = [torch.cuda.Event(), torch.cuda.Event()]
         count = [0]
 
         def launch_pipelined(c0, c1):
@@ -543,6 +568,12 @@ def run_gpu(args, dist: Dist):
             s_, co, pieces, decoded, pst, ost, dl, T, rank = views(S, c0, c1)
             rec = pieces[:, :m]
             with torch.cuda.stream(side):
+                # the address stream of set bi is free once group i-2's encode has run: written here, behind group
+                # i-1's elimination on the side stream, long before the launch stream reaches group i's encode
+                if i >= 2:
+                    side.wait_event(ev_enc[bi])
+                batch.encode_batch_prepare(s_, co, pieces, S["plan"], ctx_side)
+                ev_pl[bi].record()
                 if i >= 2:
                     side.wait_event(ev_done[bi])
                 batch.encode_batch_headers(co, pieces, ctx_side)
@@ -550,7 +581,8 @@ def run_gpu(args, dist: Dist):
                 ev_el[bi].record()
             if i >= 2:
                 torch.cuda.current_stream().wait_event(ev_done[bi])
-            batch.encode_batch_data(s_, co, pieces, ctx)
+            torch.cuda.current_stream().wait_event(ev_pl[bi])
+            batch.encode_batch_data_planned(s_, co, pieces, S["plan"], ctx)
             ev_enc[bi].record()
             with torch.cuda.stream(s_dec):
                 s_dec.wait_event(ev_enc[bi])
@@ -604,11 +636,14 @@ def run_gpu(args, dist: Dist):
     if not args.encode_only:
         for S in sets:
             ok = ok and verified(S)
-    ok = dist.allreduce(float(ok), "sum") == dist.world
     timed_enc = enc_events[skip:] or enc_events
     enc_ms = sum(a.elapsed_time(b) for a, b in timed_enc) / len(timed_enc)
     timed_dec = dec_events[skip:] or dec_events
     dec_ms = sum(a.elapsed_time(b) for a, b in timed_dec) / len(timed_dec)
+    ok_rank = dist.allgather(float(ok))
+    ok = all(v == 1.0 for v in ok_rank)
+    enc_ms_rank = dist.allgather(enc_ms)
+    dec_ms_rank = dist.allgather(dec_ms)
 
     per_rank_bytes = step_bytes(objs, k, L, n) if not args.encode_only else objs * n * encode_counter(k, L)
     total_bytes = dist.allreduce(float(per_rank_bytes * args.steps), "sum")
@@ -627,17 +662,19 @@ def run_gpu(args, dist: Dist):
     variant = VARIANTS[args.variant]
     traffic, traffic_src = pmc_traffic(variant, B, k, L, n)
     ceiling = None if args.no_ceiling else xor3_ceiling()
-    peak = ceiling["peak_T_ma_per_s"] if ceiling else None
+    live = ceiling["peak_T_ma_per_s"] if ceiling else None
     roofline = {
         "bound": "valu",
         "achieved": round(achieved, 2),
-        "peak": peak,
+        # peak = the guide's VALU issue rate (MI355X_MICROARCH.md: one wave64 instruction per 2 cycles per SIMD at
+        # 2.4 GHz, 1,024 SIMDs) x 256 GF(2^8) multiply-adds per XOR3
+        "peak": round(SPEC_PEAK_T_MA, 2),
         "unit": "T GF(2^8) multiply-adds/s",
-        "frac": round(achieved / peak, 4) if peak else None,
-        # the same against the guide's issue spec (2 cycles per wave64 VALU instruction at 2.4 GHz), not the live
-        # ceiling: the live XOR3 rate is 0.75-0.77 of spec (clock under load, 3-source issue), so frac_spec < frac
-        "peak_spec": round(SPEC_PEAK_T_MA, 2),
-        "frac_spec": round(achieved / SPEC_PEAK_T_MA, 4),
+        "frac": round(achieved / SPEC_PEAK_T_MA, 4),
+        # beside it, the live XOR3-issue ceiling measured in this run (measure/gf_ceiling.hip: independent XOR3s only,
+        # 0.75-0.77 of the spec rate -- the clock under load and three-source issue)
+        "peak_live": live,
+        "frac_live": round(achieved / live, 4) if live else None,
         "traffic": traffic,
         "traffic_source": traffic_src,
         "kernel": f"{KERNELS[variant]} (encode: {n} coded pieces x {B} objects per launch)",
@@ -699,7 +736,10 @@ def run_gpu(args, dist: Dist):
         "unit": "GiB/s",
         "n_gpus": dist.world,
         "world_size_initialised": dist.initialised_world(),
-        "process_group_backend": dist.pg.get_backend() if dist.pg else None,
+        "process_group_backend": dist.backend(),
+        "verified_per_rank": [bool(v) for v in ok_rank],
+        "kernel_ms_per_rank": [round(v, 4) for v in enc_ms_rank],
+        "decode_ms_per_rank": [round(v, 4) for v in dec_ms_rank],
         # 1: the device runs 16-byte vector memory instructions at any byte address (probed at context creation;
         # misaligned rows take the vector kernels directly), 0: they go through realigning copies
         "unaligned_vector_access": int(ctx.lib.rlnc_device_unaligned_vector_access(dist.local_rank)),

@@ -235,6 +235,19 @@ int rlnc_encode_batch_headers(rlnc_context *ctx, const uint8_t *coeffs_dev, size
                               size_t n, uint8_t *pieces_dev);
 int rlnc_encode_batch_data(rlnc_context *ctx, const uint8_t *src_dev, size_t k, size_t L, size_t num_objects,
                            const uint8_t *coeffs_dev, size_t n, uint8_t *pieces_dev);
+/* rlnc_encode_batch_data with the kernel's per-coefficient code-block address stream written ahead: _prepare runs
+ * the (coefficient-only) address launch on ITS context's stream into plan_dev (device memory of at least
+ * rlnc_encode_batch_plan_bytes bytes), e.g. on a side stream beside other work; _data_planned, with the same
+ * arguments and the same kernel variant, then runs the product without that launch (the caller orders it after the
+ * prepare, e.g. with an event).  A plan buffer serves the product it was prepared for (same buffers, shape, device,
+ * variant; the coefficients as they were at the prepare); _data_planned returns InvalidArgument for any other.
+ * Writes exactly what rlnc_encode_batch_data writes. */
+size_t rlnc_encode_batch_plan_bytes(size_t k, size_t num_objects, size_t n);
+int rlnc_encode_batch_prepare(rlnc_context *ctx, const uint8_t *src_dev, size_t k, size_t L, size_t num_objects,
+                              const uint8_t *coeffs_dev, size_t n, uint8_t *pieces_dev, void *plan_dev,
+                              size_t plan_bytes);
+int rlnc_encode_batch_data_planned(rlnc_context *ctx, const uint8_t *src_dev, size_t k, size_t L, size_t num_objects,
+                                   const uint8_t *coeffs_dev, size_t n, uint8_t *pieces_dev, const void *plan_dev);
 /* count recoded pieces per object from n received pieces: r [obj][count][n] → out [obj][count][k+L]
  * (recoder.rs:122-153; coefficient header and data are one linear combination of the full pieces). */
 int rlnc_recode_batch(rlnc_context *ctx, const uint8_t *pieces_dev, size_t k, size_t L, size_t n,

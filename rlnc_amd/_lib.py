@@ -108,6 +108,11 @@ _SIGS = {
     "rlnc_encode_batch": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, vp, C.c_size_t, vp]),
     "rlnc_encode_batch_data": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, vp, C.c_size_t, vp]),
     "rlnc_encode_batch_headers": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp]),
+    "rlnc_encode_batch_plan_bytes": (C.c_size_t, [C.c_size_t, C.c_size_t, C.c_size_t]),
+    "rlnc_encode_batch_prepare": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, vp, C.c_size_t, vp, vp,
+                                            C.c_size_t]),
+    "rlnc_encode_batch_data_planned": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, vp, C.c_size_t, vp,
+                                                 vp]),
     "rlnc_decode_batch_eliminate": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
                                               vp, vp, vp]),
     "rlnc_decode_batch_apply": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp,

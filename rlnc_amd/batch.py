@@ -78,6 +78,43 @@ def encode_batch_data(src, coeffs, out, ctx: Context | None = None) -> None:
                                          C.c_void_p(coeffs.data_ptr()), n, C.c_void_p(out.data_ptr())), ctx.lib)
 
 
+def encode_plan_bytes(k: int, nobj: int, n: int) -> int:
+    """Device bytes of an encode plan buffer (encode_batch_prepare)."""
+    from ._lib import load
+
+    return int(load().rlnc_encode_batch_plan_bytes(k, nobj, n))
+
+
+def encode_batch_prepare(src, coeffs, out, plan, ctx: Context | None = None) -> None:
+    """The code-block address stream of encode_batch_data(src, coeffs, out) written ahead into `plan` (a uint8 device
+    tensor of encode_plan_bytes bytes) on this context's stream -- e.g. a side stream, so that the encode launch
+    itself does not wait for it (encode_batch_data_planned)."""
+    nobj, k, L = src.shape
+    n = coeffs.shape[1]
+    _chk(src)
+    _chk(coeffs, (nobj, n, k))
+    _chk(out, (nobj, n, k + L))
+    _chk(plan)
+    ctx = _ctx_for(src, ctx)
+    check(ctx.lib.rlnc_encode_batch_prepare(ctx.h, C.c_void_p(src.data_ptr()), k, L, nobj,
+                                            C.c_void_p(coeffs.data_ptr()), n, C.c_void_p(out.data_ptr()),
+                                            C.c_void_p(plan.data_ptr()), plan.numel()), ctx.lib)
+
+
+def encode_batch_data_planned(src, coeffs, out, plan, ctx: Context | None = None) -> None:
+    """encode_batch_data with the address stream prepared by encode_batch_prepare (same arguments); the caller
+    orders this launch after the prepare."""
+    nobj, k, L = src.shape
+    n = coeffs.shape[1]
+    _chk(src)
+    _chk(coeffs, (nobj, n, k))
+    _chk(out, (nobj, n, k + L))
+    ctx = _ctx_for(src, ctx)
+    check(ctx.lib.rlnc_encode_batch_data_planned(ctx.h, C.c_void_p(src.data_ptr()), k, L, nobj,
+                                                 C.c_void_p(coeffs.data_ptr()), n, C.c_void_p(out.data_ptr()),
+                                                 C.c_void_p(plan.data_ptr())), ctx.lib)
+
+
 def recode_batch(pieces, r, out, k: int, ctx: Context | None = None) -> None:
     """out[o][c] = Σ_i r[o][c][i]·pieces[o][i] (coefficient header and data alike, recoder.rs:122-153)."""
     nobj, n, full = pieces.shape

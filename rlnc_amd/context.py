@@ -101,7 +101,9 @@ def stream_context(device: int, stream_handle: int) -> Context:
     # closing a context synchronises its streams and frees its workspaces, which a graph capture in progress (torch's
     # default global capture mode) forbids: evict at the next call outside a capture instead
     if len(ctxs) > STREAM_CONTEXTS_PER_THREAD and not _capturing():
-        evictable = [k for k, v in ctxs.items() if k != key and not v.graph_bound]
+        # a context whose own stream is capturing (a global-mode capture on another stream than torch's current one
+        # also forbids the synchronisation) is skipped too
+        evictable = [k for k, v in ctxs.items() if k != key and not v.graph_bound and not _stream_capturing(k[1])]
         while len(ctxs) > STREAM_CONTEXTS_PER_THREAD and evictable:
             ctxs.pop(evictable.pop(0)).close()
     return c
@@ -113,6 +115,27 @@ def _capturing() -> bool:
 
         return bool(torch.cuda.is_available() and torch.cuda.is_current_stream_capturing())
     except Exception:
+        return False
+
+
+_hip = None
+
+
+def _stream_capturing(stream_handle: int) -> bool:
+    """hipStreamIsCapturing on a raw stream handle (the HIP runtime torch has loaded); True when unsure."""
+    global _hip
+    import ctypes
+
+    try:
+        if _hip is None:
+            _hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+            _hip.hipStreamIsCapturing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+            _hip.hipStreamIsCapturing.restype = ctypes.c_int
+        st = ctypes.c_int(0)
+        if _hip.hipStreamIsCapturing(ctypes.c_void_p(stream_handle or None), ctypes.byref(st)) != 0:
+            return True
+        return st.value != 0  # hipStreamCaptureStatusNone = 0
+    except OSError:
         return False
 
 

@@ -111,8 +111,15 @@ struct CallWs {
     DevBuf pc_part, pc_pcount;  // split products (piece.hpp): partial slabs and per-block counters
     size_t pc_pcount_words = 0;  // zeroed words of pc_pcount
     uint32_t epoch = 0;
+    // large copy-outs to host (Decoder::get_decoded_data): a ring of pinned chunks the DMA fills while host threads
+    // copy the previous chunks into the caller's buffer (engine.cpp copy_out)
+    static constexpr int kOutRing = 3;
+    PinBuf pin_out;
+    hipEvent_t out_ev[kOutRing] = {};
     CallWs() { pc_coef.flags = pc_out.flags = pc_flag.flags = hipHostMallocCoherent; }
     ~CallWs() {
+        for (hipEvent_t e : out_ev)
+            if (e) (void)hipEventDestroy(e);
         if (ev) (void)hipEventDestroy(ev);
         if (stream) (void)hipStreamDestroy(stream);
     }

@@ -23,6 +23,7 @@
 #include "context.hpp"
 #include "elimination.hpp"
 #include "gf256.hpp"
+#include "host_copy.hpp"
 #include "kernels.hpp"
 #include "piece.hpp"
 
@@ -135,11 +136,13 @@ rlnc::MatmulParams encoder_params(const rlnc_encoder *e, const uint8_t *cv_dev, 
 }
 
 // ---- the call-latency path of the object API (piece.hip) ----------------------------------------------------------
-// Decoder::get_decoded_data takes it up to this much output and this many multiply-adds (the kernel reads every
+// Encoder::code_with_buf / Recoder::recode_with_buf / Decoder::get_decoded_data take it up to this much output (a
+// pooled workspace keeps a coherent pinned output buffer as large as the largest piece it produced), the decoder up to
+// this many multiply-adds too (the kernel reads every
 // source chunk once per output row, so larger products go to the batch kernels instead; its 16-byte write-through
 // stores across PCIe run at ~10 GB/s, so outputs of many MiB come back faster as one DMA: 16 MiB objects 0.63 ms that
 // way against 0.92 through the kernel, 1 MiB objects 0.11 ms against 0.22 -- profiles/r04_object_api_bench_full_v1)
-constexpr size_t kPieceDecodeMaxBytes = size_t(4) << 20;
+constexpr size_t kPieceMaxBytes = size_t(4) << 20;
 constexpr size_t kPieceDecodeMaxMacs = size_t(1) << 31;
 
 // rows of `width` bytes at a 16-byte-aligned stride with room for the last slot's whole 16 bytes
@@ -263,7 +266,12 @@ int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t
     p.chunk_blocks = piece_chunk_blocks();  // 64 KiB of a row per flag: the host copies one while the device writes on
     const size_t chunks = size_t(rlnc::piece_chunks(p));
     if (int st = ws->pc_out.ensure(n_out * size_t(p.out_row))) return st;
-    if (int st = ws->pc_flag.ensure(chunks * 4)) return st;
+    if (chunks * 4 > ws->pc_flag.cap) {
+        // completion is "flag == epoch" and every workspace counts its epochs from 1: a freshly allocated pinned
+        // buffer may hold another (freed) workspace's flag values, so it starts zeroed (epochs are never 0)
+        if (int st = ws->pc_flag.ensure(chunks * 4)) return st;
+        std::memset(ws->pc_flag.p, 0, ws->pc_flag.cap);
+    }
     if (chunks > ws->pc_count_words) {
         if (int st = ws->pc_count.ensure(chunks * 4)) return st;
         HIP_TRY(hipMemsetAsync(ws->pc_count.p, 0, chunks * 4, ws->stream));
@@ -638,7 +646,7 @@ int rlnc_encoder_code_with_coding_vector(rlnc_encoder *e, const uint8_t *cv, siz
     int st = ctx->activate();
     if (st || (st = ctx->note_capture())) return st;
     Lease ws(ctx);
-    if (piece_eligible(e->src, e->stride, e->L)) {
+    if (e->L <= kPieceMaxBytes && piece_eligible(e->src, e->stride, e->L)) {
         // an owned source is immutable after Encoder::new (its upload synchronised); a borrowed one is ordered after
         // the context stream's work
         if ((st = ws.acquire(!e->owned))) return st;
@@ -765,7 +773,7 @@ int rlnc_recoder_recode_with_buf(rlnc_recoder *r, const uint8_t *rnd, size_t n_r
     int st = ctx->activate();
     if (st || (st = ctx->note_capture())) return st;
     Lease ws(ctx);
-    if (piece_eligible(r->pieces, r->stride, r->full)) {
+    if (r->full <= kPieceMaxBytes && piece_eligible(r->pieces, r->stride, r->full)) {
         // the received pieces are immutable after Recoder::new (its upload synchronised): no ordering
         if ((st = ws.acquire(false))) return st;
         return piece_call(ws.ws.get(), r->pieces, r->stride, r->n, r->full, rnd, r->n, 1, full, r->full);
@@ -967,6 +975,46 @@ static int decoder_apply(rlnc_decoder *d, CallWs *ws, uint8_t *out_dev) {
     return d->ctx->matmul(p, ws->stream, ws->idx, false);
 }
 
+namespace {
+// Device -> caller host memory for large outputs: chunks DMA'd into a ring of pinned buffers (ws->pin_out), each
+// copied into dst by the host copy pool (host_copy.hpp) while the next chunks are in flight.  The caller's buffer is
+// typically fresh (the reference returns a new vec![0u8; k·L], decoder.rs:141-142): the pool's threads also share its
+// page faults, which one thread paid alone in the runtime's pageable copy (round 4: 5.8 ms for 32 MiB).
+constexpr size_t kOutChunk = size_t(4) << 20;
+constexpr size_t kOutParallelMin = size_t(8) << 20;  // below this one pageable DMA is as fast (profiles/r05_copyout*)
+
+int copy_out(CallWs *ws, uint8_t *dst, const uint8_t *src_dev, size_t n) {
+    const int threads = copy_threads();
+    if (n < kOutParallelMin || threads <= 1) {
+        HIP_TRY(hipMemcpyAsync(dst, src_dev, n, hipMemcpyDeviceToHost, ws->stream));
+        HIP_TRY(hipStreamSynchronize(ws->stream));
+        return RLNC_OK;
+    }
+    constexpr int R = CallWs::kOutRing;
+    if (int st = ws->pin_out.ensure(size_t(R) * kOutChunk)) return st;
+    for (hipEvent_t &e : ws->out_ev)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    uint8_t *stage = ws->pin_out.as<uint8_t>();
+    const size_t chunks = (n + kOutChunk - 1) / kOutChunk;
+    auto issue = [&](size_t c) -> int {
+        const size_t off = c * kOutChunk, len = std::min(kOutChunk, n - off);
+        HIP_TRY(hipMemcpyAsync(stage + (c % R) * kOutChunk, src_dev + off, len, hipMemcpyDeviceToHost, ws->stream));
+        HIP_TRY(hipEventRecord(ws->out_ev[c % R], ws->stream));
+        return RLNC_OK;
+    };
+    for (size_t c = 0; c < std::min<size_t>(R, chunks); ++c)
+        if (int st = issue(c)) return st;
+    for (size_t c = 0; c < chunks; ++c) {
+        HIP_TRY(hipEventSynchronize(ws->out_ev[c % R]));
+        const size_t off = c * kOutChunk, len = std::min(kOutChunk, n - off);
+        par_copy(dst + off, stage + (c % R) * kOutChunk, len, threads);
+        if (c + R < chunks)
+            if (int st = issue(c + R)) return st;
+    }
+    return RLNC_OK;
+}
+}  // namespace
+
 int rlnc_decoder_get_decoded_data(rlnc_decoder *d, uint8_t *out, size_t cap, size_t *out_len) {
     CHECK_ARG(d != nullptr);
     if (!d->elim->decoded()) return RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;  // decoder.rs:137-139
@@ -975,7 +1023,7 @@ int rlnc_decoder_get_decoded_data(rlnc_decoder *d, uint8_t *out, size_t cap, siz
     if (st) return st;
     Lease ws(d->ctx);
     const size_t slots = d->elim->slots();
-    if (d->k * round16(d->L) <= kPieceDecodeMaxBytes && d->k * slots * d->L <= kPieceDecodeMaxMacs &&
+    if (d->k * round16(d->L) <= kPieceMaxBytes && d->k * slots * d->L <= kPieceDecodeMaxMacs &&
         piece_eligible(d->store, d->stride, d->L)) {
         // T (k x slots) is read by the kernel from pinned memory and the rows land in pinned memory, copied into out
         // chunk by chunk as the device finishes them.  Store rows never stored are referenced by zero columns of T
@@ -990,8 +1038,7 @@ int rlnc_decoder_get_decoded_data(rlnc_decoder *d, uint8_t *out, size_t cap, siz
     } else {
         if ((st = ws.acquire()) || (st = ws->out.ensure(d->k * d->L))) return st;
         if ((st = decoder_apply(d, ws.ws.get(), ws->out.as<uint8_t>()))) return st;
-        HIP_TRY(hipMemcpyAsync(out, ws->out.p, d->k * d->L, hipMemcpyDeviceToHost, ws->stream));
-        HIP_TRY(hipStreamSynchronize(ws->stream));
+        if ((st = copy_out(ws.ws.get(), out, ws->out.as<uint8_t>(), d->k * d->L))) return st;
     }
     // get_final_data_len — decoder.rs:162-177: last nonzero byte must be the 0x81 marker, not at 0
     size_t n = d->k * d->L;
@@ -1027,15 +1074,8 @@ int rlnc_decoder_get_decoded_data_device(rlnc_decoder *d, uint8_t *out_dev, size
 // ------------------------------------------------------------------------------------------------------
 // batch API
 // ------------------------------------------------------------------------------------------------------
-static int encode_batch_impl(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t nobj,
-                             const uint8_t *coeffs, size_t n, uint8_t *pieces, bool headers) {
-    CHECK_ARG(ctx != nullptr);
-    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
-    if (L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;
-    if (n == 0 || nobj == 0) return RLNC_OK;
-    CHECK_ARG(src && coeffs && pieces && n <= 0x7FFFFFFF && k <= 0x7FFFFFFF && nobj <= 0x7FFFFFFF);
-    int st = ctx->activate();
-    if (st || (st = ctx->note_capture())) return st;
+static rlnc::MatmulParams encode_batch_params(const uint8_t *src, size_t k, size_t L, size_t nobj,
+                                              const uint8_t *coeffs, size_t n, uint8_t *pieces, bool headers) {
     const int64_t full = int64_t(k + L);
     rlnc::MatmulParams p{};
     p.in = src;
@@ -1054,6 +1094,58 @@ static int encode_batch_impl(rlnc_context *ctx, const uint8_t *src, size_t k, si
     p.n_in = int(k);
     p.width = int64_t(L);
     p.n_obj = int(nobj);
+    return p;
+}
+
+// Block-address streams written ahead by rlnc_encode_batch_prepare (any context, any stream), by buffer: the product
+// they were written for and their layout.  rlnc_encode_batch_data_planned uses one only for exactly that product.
+struct EncodePlanRec {
+    int device;
+    const uint8_t *src, *coeffs;
+    uint8_t *pieces;
+    size_t k, L, nobj, n;
+    int variant;
+    rlnc::BsjStreamPlan plan;
+};
+static std::mutex g_plan_mu;
+static std::vector<std::pair<const void *, EncodePlanRec>> g_plans;  // (buffer, record), most recent last
+constexpr size_t kPlanRecs = 64;
+
+static int encode_batch_impl(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t nobj,
+                             const uint8_t *coeffs, size_t n, uint8_t *pieces, bool headers,
+                             const void *plan_buf = nullptr) {
+    CHECK_ARG(ctx != nullptr);
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
+    if (L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;
+    if (n == 0 || nobj == 0) return RLNC_OK;
+    CHECK_ARG(src && coeffs && pieces && n <= 0x7FFFFFFF && k <= 0x7FFFFFFF && nobj <= 0x7FFFFFFF);
+    int st = ctx->activate();
+    if (st || (st = ctx->note_capture())) return st;
+    rlnc::MatmulParams p = encode_batch_params(src, k, L, nobj, coeffs, n, pieces, headers);
+    if (plan_buf) {
+        EncodePlanRec rec{};
+        bool found = false;
+        {
+            std::lock_guard<std::mutex> lock(g_plan_mu);
+            for (auto it = g_plans.rbegin(); it != g_plans.rend(); ++it)
+                if (it->first == plan_buf) {
+                    rec = it->second;
+                    found = true;
+                    break;
+                }
+        }
+        if (!found || rec.device != ctx->device || rec.src != src || rec.coeffs != coeffs || rec.pieces != pieces ||
+            rec.k != k || rec.L != L || rec.nobj != nobj || rec.n != n || rec.variant != int(ctx->variant))
+            return set_error(RLNC_ERR_INVALID_ARGUMENT,
+                             "encode plan %p was not prepared for this product (same buffers, shape, device and kernel "
+                             "variant): call rlnc_encode_batch_prepare with the arguments of this call",
+                             plan_buf);
+        if (rec.plan.tile_rows > 0) {
+            p.bsj_stream = plan_buf;
+            p.bsj_stream_rows = rec.plan.tile_rows;
+            p.bsj_stream_abs = rec.plan.abs;
+        }
+    }
     return ctx->matmul(p);
 }
 
@@ -1065,6 +1157,44 @@ int rlnc_encode_batch(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L,
 int rlnc_encode_batch_data(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t nobj,
                            const uint8_t *coeffs, size_t n, uint8_t *pieces) {
     return encode_batch_impl(ctx, src, k, L, nobj, coeffs, n, pieces, false);
+}
+
+size_t rlnc_encode_batch_plan_bytes(size_t k, size_t nobj, size_t n) {
+    if (k == 0 || n == 0 || nobj == 0 || k > 0x7FFFFFFF || n > 0x7FFFFFFF || nobj > 0x7FFFFFFF) return 0;
+    return rlnc::bsj_stream_bytes_bound(int(nobj), int(n), int(k));
+}
+
+int rlnc_encode_batch_prepare(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t nobj,
+                              const uint8_t *coeffs, size_t n, uint8_t *pieces, void *plan_buf, size_t plan_bytes) {
+    CHECK_ARG(ctx != nullptr);
+    if (k == 0) return RLNC_ERR_PIECE_COUNT_ZERO;
+    if (L == 0) return RLNC_ERR_PIECE_LENGTH_ZERO;
+    if (n == 0 || nobj == 0) return RLNC_OK;
+    CHECK_ARG(src && coeffs && pieces && plan_buf && n <= 0x7FFFFFFF && k <= 0x7FFFFFFF && nobj <= 0x7FFFFFFF);
+    CHECK_ARG(plan_bytes >= rlnc_encode_batch_plan_bytes(k, nobj, n));
+    int st = ctx->activate();
+    if (st || (st = ctx->note_capture())) return st;
+    const rlnc::MatmulParams p = encode_batch_params(src, k, L, nobj, coeffs, n, pieces, false);
+    rlnc::BsjStreamPlan plan;
+    // the row-split tuning knob launches per row range, each with its own stream: nothing to write ahead
+    if (!(ctx->max_tile_rows > 0 && p.n_out > ctx->max_tile_rows))
+        HIP_TRY(rlnc::launch_bsj_stream(p, ctx->variant, ctx->stream, plan_buf, plan_bytes, plan));
+    EncodePlanRec rec{ctx->device, src, coeffs, pieces, k, L, nobj, n, int(ctx->variant), plan};
+    std::lock_guard<std::mutex> lock(g_plan_mu);
+    for (auto it = g_plans.begin(); it != g_plans.end(); ++it)
+        if (it->first == plan_buf) {
+            g_plans.erase(it);
+            break;
+        }
+    if (g_plans.size() >= kPlanRecs) g_plans.erase(g_plans.begin());
+    g_plans.emplace_back(plan_buf, rec);
+    return RLNC_OK;
+}
+
+int rlnc_encode_batch_data_planned(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t nobj,
+                                   const uint8_t *coeffs, size_t n, uint8_t *pieces, const void *plan_buf) {
+    CHECK_ARG(plan_buf != nullptr);
+    return encode_batch_impl(ctx, src, k, L, nobj, coeffs, n, pieces, false, plan_buf);
 }
 
 int rlnc_encode_batch_headers(rlnc_context *ctx, const uint8_t *coeffs, size_t k, size_t L, size_t nobj, size_t n,

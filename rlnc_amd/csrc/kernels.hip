@@ -651,7 +651,8 @@ hipError_t bsj_prepare(const MatmulParams &p, hipStream_t s, void *scratch, size
     b.col_blocks = int(b.full / kBsjColBlock);
     b.total = int64_t(p.n_obj) * b.row_tiles * b.col_blocks;
     if (b.total > 0x7FFFFFFFLL || p.n_obj > 65535) return hipErrorInvalidValue;
-    if (!abs && p.bsj_stream != nullptr && p.bsj_stream_rows == tile_rows) {  // written by the elimination already
+    if (p.bsj_stream != nullptr && p.bsj_stream_rows == tile_rows && (p.bsj_stream_abs != 0) == abs) {
+        // written already: by the small-object elimination (4-byte offsets) or by launch_bsj_stream ahead
         b.stream = const_cast<void *>(p.bsj_stream);
         return hipSuccess;
     }
@@ -1298,6 +1299,32 @@ static bool realign_plan(const MatmulParams &p, MatmulVariant v, RealignPlan &r)
     r.in_bytes = r.in_mis ? size_t(objs) * p.n_in * r.lr : 0;
     r.out_bytes = r.out_mis ? size_t(objs) * p.n_out * r.lr : 0;
     return true;
+}
+
+size_t bsj_stream_bytes_bound(int n_obj, int n_out, int n_in) {
+    // tiles x tile_rows < n_out + 64 rows, 8 bytes an entry, + the main loop's one-source overrun
+    return size_t(n_obj) * size_t(n_out + 64) * size_t(n_in) * 8 + 512;
+}
+
+hipError_t launch_bsj_stream(const MatmulParams &p, MatmulVariant v, hipStream_t s, void *buf, size_t bytes,
+                             BsjStreamPlan &plan) {
+    plan = BsjStreamPlan{};
+    if (p.n_out <= 0 || p.width <= 0 || p.n_obj <= 0 || p.n_in <= 0 || !shipped_variant(v) || !jump_variant(v))
+        return hipSuccess;
+    RealignPlan r;
+    if (realign_plan(p, v, r)) return hipSuccess;  // the realigned chunks write their own streams
+    const bool aligned = matmul_aligned(p);
+    if (aligned && p.n_out <= 3 && p.width >= kColBlock) return hipSuccess;  // the single-pass stream kernel
+    if (!bsj_eligible(p, aligned)) return hipSuccess;
+    const bool share = v == MatmulVariant::BitSlicedJumpShared || v == MatmulVariant::BitSlicedJumpShared8;
+    const bool wide = v == MatmulVariant::BitSlicedJumpShared8;
+    MatmulParams q = p;
+    q.bsj_stream = nullptr;
+    BsjPlan b;
+    if (hipError_t e = bsj_prepare(q, s, buf, bytes, share, wide, b); e != hipSuccess) return e;
+    plan.tile_rows = kBsjWaveRows * b.waves;
+    plan.abs = (b.share && b.waves >= 4) ? 1 : 0;  // the shared programs (4 and 8 waves) call absolute addresses
+    return hipSuccess;
 }
 
 size_t matmul_scratch_bytes(const MatmulParams &p, MatmulVariant v) {

@@ -32,6 +32,9 @@ struct MatmulParams {
     // the product takes the 1- or 2-wave bit-sliced program with exactly those tiles, else ignored
     const void *bsj_stream = nullptr;
     int bsj_stream_rows = 0;
+    // 1: bsj_stream holds the shared programs' 8-byte absolute block addresses instead (launch_bsj_stream, written
+    // ahead on another stream: the encode's block-address stream off the launch stream's critical path)
+    int bsj_stream_abs = 0;
 };
 
 enum class MatmulVariant : int {
@@ -84,6 +87,17 @@ bool bsj_eligible_public(const MatmulParams &p);
 size_t bsj_scratch_bytes_public(const MatmulParams &p, bool wide);
 hipError_t bsj_prepare(const MatmulParams &p, hipStream_t s, void *scratch, size_t scratch_bytes, bool share, bool wide,
                        BsjPlan &b);
+// The block-address stream of launch_matmul(p, v)'s bit-sliced product written ahead into buf (one offset launch on s),
+// for a later launch_matmul of the same p with bsj_stream = buf, bsj_stream_rows = tile_rows, bsj_stream_abs = abs.
+// tile_rows = 0: that product takes no stream (another kernel, or realigned operands) and nothing is launched.
+struct BsjStreamPlan {
+    int tile_rows = 0;
+    int abs = 0;
+};
+hipError_t launch_bsj_stream(const MatmulParams &p, MatmulVariant v, hipStream_t s, void *buf, size_t bytes,
+                             BsjStreamPlan &plan);
+// an upper bound of launch_bsj_stream's buffer for n_obj objects of n_out x n_in coefficients
+size_t bsj_stream_bytes_bound(int n_obj, int n_out, int n_in);
 
 // ---- ragged batches: one launch per kernel stage over objects of different shapes (wire.hip) -----------------
 // One object's part of a ragged matmul launch (device-side descriptor table, 120 bytes).  Objects are ordered by

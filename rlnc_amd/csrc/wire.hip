@@ -88,7 +88,11 @@ int upload_table(rlnc_context *ctx, const void *host, size_t bytes, void **dev) 
     PinBuf &pin = ctx->pin_tab[r];
     hipEvent_t &ev = ctx->tab_ev[r];
     if (ev) HIP_TRY(hipEventSynchronize(ev));
-    if ((st = ctx->grow(pin, need)) || (st = ctx->grow(ctx->ws_tab, need))) return st;
+    // the eager staging buffer and device table are never referenced by a captured graph (captured calls use the
+    // capture arena above), so they grow even on a graph-bound context; each ring slot grows on its own first use
+    // of a larger table.  The device table may still be read by earlier eager launches: drain the stream first.
+    if (need > ctx->ws_tab.cap) HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if ((st = pin.ensure(need)) || (st = ctx->ws_tab.ensure(need))) return st;
     std::memcpy(pin.p, host, bytes);
     if (need / 16 > 0xFFFFFF00u) return set_error(RLNC_ERR_INVALID_ARGUMENT, "descriptor table too large");
     const uint32_t n16 = uint32_t(need / 16);

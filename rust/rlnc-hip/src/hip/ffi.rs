@@ -292,6 +292,30 @@ unsafe extern "C" {
         n: usize,
         pieces_dev: *mut u8,
     ) -> c_int;
+    pub fn rlnc_encode_batch_plan_bytes(k: usize, num_objects: usize, n: usize) -> usize;
+    pub fn rlnc_encode_batch_prepare(
+        ctx: *mut rlnc_context,
+        src_dev: *const u8,
+        k: usize,
+        L: usize,
+        num_objects: usize,
+        coeffs_dev: *const u8,
+        n: usize,
+        pieces_dev: *mut u8,
+        plan_dev: *mut c_void,
+        plan_bytes: usize,
+    ) -> c_int;
+    pub fn rlnc_encode_batch_data_planned(
+        ctx: *mut rlnc_context,
+        src_dev: *const u8,
+        k: usize,
+        L: usize,
+        num_objects: usize,
+        coeffs_dev: *const u8,
+        n: usize,
+        pieces_dev: *mut u8,
+        plan_dev: *const c_void,
+    ) -> c_int;
     pub fn rlnc_recode_batch(
         ctx: *mut rlnc_context,
         pieces_dev: *const u8,

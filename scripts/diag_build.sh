@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Diagnostic library builds without diagnostic code in the shipped sources: copy rlnc_amd/csrc into <out>/src/csrc,
-# substitute files (name=path: e.g. a generated bitslice_jump.inc variant, or rref.hip=scripts/diag/rref_profile.hip),
+# substitute files (name=path: e.g. a generated bitslice_jump.inc variant, or kernels.hip=<variant>),
 # build <out>/librlnc_hip.so there (AB=1: the A/B library, make ab), extra compiler flags after --.
 #   scripts/diag_build.sh build/diag_x bitslice_jump.inc=build/diag_x/bitslice_jump.inc -- -DFOO
 set -eu

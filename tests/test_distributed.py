@@ -1,6 +1,7 @@
 """CPU (gloo, world_size 2): the multi-rank path of bench.py — barrier-bracketed timing, max-over-ranks
 elapsed time and summed bytes — with the oracle as the per-rank work (objects sharded, no data-path
-collective).  Runs here without a GPU; the GPU bench uses the same Dist/timed_loop code over RCCL."""
+collective).  Runs here without a GPU; the GPU bench uses the same Dist/timed_loop code and the same gloo group at
+every N (the data path has no collective: DESIGN.md §6)."""
 import os
 import socket
 
@@ -25,7 +26,7 @@ def _worker(rank, world, port, q):
     import bench
     from oracle.oracle import Oracle, OracleDecoder
 
-    d = bench.Dist().init("gloo")
+    d = bench.Dist().init()
     orc = Oracle()
     k, L, n, m, B = 8, 512, 12, 8, 3
     rng = np.random.default_rng(100 + rank)  # each rank owns different objects
@@ -85,7 +86,7 @@ def test_step_bytes_matches_reference_counters():
 def test_self_spawn_two_ranks_gloo():
     """`bench.py --gpus 2` with no launcher starts its own 2 ranks (fresh interpreters, RANK/WORLD_SIZE/MASTER_*
     set, rendezvous on 127.0.0.1) and rank 0 prints the one JSON line; here each rank's work is the C oracle
-    over gloo (--workload oracle-cpu), the GPU bench takes the same path over RCCL."""
+    over gloo (--workload oracle-cpu), the GPU bench takes the same path and the same group."""
     import json
     import subprocess
     import sys
@@ -101,6 +102,7 @@ def test_self_spawn_two_ranks_gloo():
     assert len(lines) == 1, r.stdout  # rank 0 only
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["steps"] == 3 and res["verified"]
+    assert res["verified_per_rank"] == [True, True]
     assert res["world_size_initialised"] == 2  # torch.distributed.get_world_size() after init_process_group
     assert res["total_bytes"] == 2 * bench.step_bytes(3, 8, 512, 12) * 3
     assert abs(res["value"] - res["total_bytes"] / res["elapsed_s"] / bench.GIB) < 1e-3
@@ -167,3 +169,33 @@ def test_single_rank_initialises_a_group():
     assert r.returncode == 0, r.stdout + r.stderr
     res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert res["n_gpus"] == 1 and res["world_size_initialised"] == 1
+
+
+def _line(args):
+    import json
+    import subprocess
+    import sys
+
+    import bench
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py")] + args,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+
+
+def test_same_process_group_backend_at_every_n():
+    """A scaling curve compares like with like: the N = 1 and N = 2 lines report the same process-group backend
+    (gloo: barrier and scalar results on the host, no RCCL streams beside the pipeline's), and the GPU run takes
+    its group from the same Dist.init() as the oracle harness."""
+    import inspect
+
+    import bench
+
+    one = _line(["--workload", "oracle-cpu", "--steps", "2", "--warmup", "1"])
+    two = _line(["--gpus", "2", "--workload", "oracle-cpu", "--steps", "2", "--warmup", "1"])
+    assert one["process_group_backend"] == two["process_group_backend"] == bench.HARNESS_BACKEND == "gloo"
+    assert one["verified_per_rank"] == [True] and two["verified_per_rank"] == [True, True]
+    src = inspect.getsource(bench.run_gpu)
+    assert "dist.init()" in src and "nccl" not in src

@@ -126,7 +126,8 @@ def pad(arr):
 
 X = pad_set()
 A = decode_set()
-pad(X[2])  # eager warm-up: workspaces, the capture arena, the block-table probe
+if WARM_PAD:
+    pad(X[2])  # eager warm-up: workspaces, the capture arena, the block-table probe
 batch.decode_ragged(A[0], ctx)
 torch.cuda.synchronize()
 s = torch.cuda.Stream()
@@ -141,6 +142,12 @@ B_ = decode_set()
 pad(Y[2])
 resB = batch.decode_ragged(B_[0], ctx)
 torch.cuda.synchronize()
+for _ in range(EXTRA_DECODES):  # more eager calls: the staging ring rotates onto slots the warm-up never grew
+    C_ = decode_set()
+    batch.decode_ragged(C_[0], ctx)
+    torch.cuda.synchronize()
+    for (pc, k, dec), src in zip(C_[0], C_[1]):
+        assert np.array_equal(dec.cpu().numpy(), src), "extra eager ragged decode"
 for (n, k), d, o in zip(shapes, Y[0], Y[1]):
     assert np.array_equal(o.cpu().numpy(), orc.pad(d.cpu().numpy(), k).reshape(-1)), "eager pad"
 for (pc, k, dec), src in zip(B_[0], B_[1]):
@@ -161,8 +168,13 @@ print("tables ok")
 """
 
 
-def test_descriptor_tables_survive_other_eager_calls_before_replay():
-    code = CHILD_TABLES.replace("ROOT", repr(ROOT))
+@pytest.mark.parametrize("warm_pad,extra", [(True, 0), (False, 2)], ids=["pad+decode-warmup", "decode-warmup+2-eager"])
+def test_descriptor_tables_survive_other_eager_calls_before_replay(warm_pad, extra):
+    """The capture's tables live in the capture arena; eager calls after the capture stage through the pinned ring,
+    whose slots grow on their own first use even on a graph-bound context (with the warm-up a single
+    ragged decode, later eager decodes land on ring slots that were never grown)."""
+    code = CHILD_TABLES.replace("ROOT", repr(ROOT)).replace("WARM_PAD", repr(warm_pad)).replace(
+        "EXTRA_DECODES", str(extra))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "tables ok" in r.stdout

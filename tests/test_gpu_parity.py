@@ -878,3 +878,47 @@ def test_decode_two_pass_beyond_one_wave_row(ctx, path):
         assert S[ost[o]] == S[st], o
     assert all(S[x] == "ReceivedAllPieces" for x in pst[0, first:])
     assert (pst[4] == 0).sum() == k and (pst[6] == 0).sum() < k
+
+
+@pytest.mark.parametrize("variant", [8, 7, 6])
+@pytest.mark.parametrize("k,L,n", [(32, 4096 * 2, 64), (32, 4096 * 3 + 17, 40), (16, 8192, 12), (8, 4096, 2),
+                                   (20, 3000, 24)])
+def test_encode_plan_written_ahead(orc, variant, k, L, n):
+    """rlnc_encode_batch_prepare on a second context / stream writes the code-block address stream ahead;
+    rlnc_encode_batch_data_planned (ordered after it by an event) writes exactly what encode_batch does, checked
+    against the oracle (encoder.rs:128-144) -- for the 8-wave absolute-address program, the 4-wave one, the
+    unshared 1- / 2-wave ones, the single-pass kernel (n = 2: no stream) and narrow shapes (perm kernel: no
+    stream).  A plan is refused for any other product (another coefficient buffer)."""
+    import torch
+
+    import rlnc_amd
+    from rlnc_amd import batch
+    from rlnc_amd.errors import RLNCError
+
+    rng = np.random.default_rng(k * 131 + n + variant)
+    nobj = 3
+    src_h = rng.integers(0, 256, (nobj, k, L), dtype=np.uint8)
+    co_h = rng.integers(0, 256, (nobj, n, k), dtype=np.uint8)
+    src, co = dev(src_h), dev(co_h)
+    c1, c2 = rlnc_amd.Context(0), rlnc_amd.Context(0)
+    for c in (c1, c2):
+        c.set_kernel_variant(variant)
+    plan = torch.zeros(batch.encode_plan_bytes(k, nobj, n), dtype=torch.uint8, device="cuda:0")
+    pieces = torch.zeros((nobj, n, k + L), dtype=torch.uint8, device="cuda:0")
+    side = torch.cuda.Stream()
+    ev = torch.cuda.Event()
+    with torch.cuda.stream(side):
+        batch.encode_batch_prepare(src, co, pieces, plan, c2)
+        ev.record()
+    batch.encode_batch_headers(co, pieces, c1)
+    torch.cuda.current_stream().wait_event(ev)
+    batch.encode_batch_data_planned(src, co, pieces, plan, c1)
+    torch.cuda.synchronize()
+    got = host(pieces)
+    for o in range(nobj):
+        assert np.array_equal(got[o], orc.encode(src_h[o], co_h[o])), o
+    other = co.clone()
+    with pytest.raises(RLNCError):
+        batch.encode_batch_data_planned(src, other, pieces, plan, c1)
+    c1.close()
+    c2.close()
