@@ -8,8 +8,11 @@
 // (encoder.rs:248, recoder.rs:131).
 #pragma once
 
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
+#include <new>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -100,6 +103,46 @@ inline rlnc_context *context() {
     return h.c;
 }
 
+// The allocator of Bytes: calloc'd storage, and value-initialisation of its bytes is a no-op -- they are zero
+// already.  That is what the reference's `vec![0u8; n]` is (alloc_zeroed = calloc: a large buffer is a fresh mapping
+// whose pages are zeroed lazily, on first write), where a std::vector<uint8_t>(n) would memset every byte on the
+// calling thread first (32 MiB: most of a large decode's get_decoded_data).  Caveat: growing a Bytes
+// that was shrunk does not re-zero the bytes it had before.
+template <class T>
+struct ZeroedAlloc {
+    using value_type = T;
+    ZeroedAlloc() = default;
+    template <class U>
+    ZeroedAlloc(const ZeroedAlloc<U> &) noexcept {}
+    T *allocate(size_t n) {
+        if (void *p = std::calloc(n ? n : 1, sizeof(T))) return static_cast<T *>(p);
+        throw std::bad_alloc();
+    }
+    void deallocate(T *p, size_t) noexcept { std::free(p); }
+    template <class U>
+    void construct(U *) noexcept {}  // value-initialised = the calloc'd zero
+    template <class U, class... A>
+    void construct(U *p, A &&...a) {
+        ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+    }
+    template <class U>
+    bool operator==(const ZeroedAlloc<U> &) const noexcept {
+        return true;
+    }
+    template <class U>
+    bool operator!=(const ZeroedAlloc<U> &) const noexcept {
+        return false;
+    }
+};
+
+using ZBytes = std::vector<uint8_t, ZeroedAlloc<uint8_t>>;
+inline bool operator==(const ZBytes &a, const std::vector<uint8_t> &b) {
+    return a.size() == b.size() && std::equal(a.begin(), a.end(), b.begin());
+}
+inline bool operator==(const std::vector<uint8_t> &a, const ZBytes &b) { return b == a; }
+inline bool operator!=(const ZBytes &a, const std::vector<uint8_t> &b) { return !(a == b); }
+inline bool operator!=(const std::vector<uint8_t> &a, const ZBytes &b) { return !(b == a); }
+
 template <class H, void (*Free)(H *)>
 struct Handle {
     H *h = nullptr;
@@ -128,6 +171,9 @@ H *clone_handle(int (*fn)(const H *, H **), const H *h) {
 }  // namespace detail
 
 namespace full {
+
+// Decoder::get_decoded_data's result: a byte vector allocated zeroed like the reference's vec![0u8; n]
+using Bytes = detail::ZBytes;
 
 // encoder.rs:19-270
 class Encoder {
@@ -199,8 +245,8 @@ class Decoder {
     size_t get_received_piece_count() const { return rlnc_decoder_get_received_piece_count(h_.h); }
     size_t get_useful_piece_count() const { return rlnc_decoder_get_useful_piece_count(h_.h); }
     size_t get_remaining_piece_count() const { return rlnc_decoder_get_remaining_piece_count(h_.h); }
-    Result<std::vector<uint8_t>> get_decoded_data() {  // decoder.rs:136-159
-        std::vector<uint8_t> out(get_num_pieces_coded_together() * get_piece_byte_len());
+    Result<Bytes> get_decoded_data() {  // decoder.rs:136-159
+        Bytes out(get_num_pieces_coded_together() * get_piece_byte_len());
         size_t n = 0;
         auto r = detail::status(rlnc_decoder_get_decoded_data(h_.h, out.data(), out.size(), &n));
         if (r.is_err()) return r.error();

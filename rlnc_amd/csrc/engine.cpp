@@ -4,6 +4,7 @@
 // pieces runs on the device through the kernels of kernels.hip; the host only runs the k×(k+slots)
 // coefficient elimination of the decoder (elimination.hpp).
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -983,6 +984,45 @@ namespace {
 constexpr size_t kOutChunk = size_t(4) << 20;
 constexpr size_t kOutParallelMin = size_t(8) << 20;  // below this one pageable DMA is as fast (profiles/r05_copyout*)
 
+// RLNC_COPY_TRACE=1 (diagnostic, read once): per-call host time of copy_out's phases, medians on stderr at exit
+struct CopyTrace {
+    bool on = [] {
+        const char *e = getenv("RLNC_COPY_TRACE");
+        return e && atoi(e) != 0;
+    }();
+    std::mutex mu;
+    std::vector<float> total, wait, copy, first;  // us per call
+    void add(float t, float w, float c, float f) {
+        std::lock_guard<std::mutex> lock(mu);
+        total.push_back(t);
+        wait.push_back(w);
+        copy.push_back(c);
+        first.push_back(f);
+    }
+    ~CopyTrace() {
+        if (on && !total.empty())
+            std::fprintf(stderr, "{\"copy_trace\": {\"calls\": %zu, \"median_total_us\": %.1f, \"median_event_wait_us\": %.1f, "
+                                 "\"median_host_copy_us\": %.1f, \"median_first_chunk_wait_us\": %.1f}}\n",
+                         total.size(), PieceTrace::med(total), PieceTrace::med(wait), PieceTrace::med(copy),
+                         PieceTrace::med(first));
+    }
+};
+CopyTrace g_copy_trace;
+
+// The whole 2 MiB-aligned pages inside dst[0, n) may be backed by transparent huge pages (a hint, where the host's
+// THP mode is "madvise"): a fresh buffer then faults in 2 MiB at a time instead of 4 KiB.  Only pages that lie entirely
+// inside the caller's output buffer are advised.  RLNC_COPY_HUGEPAGE=0 (A/B knob, read once) turns it off.
+void advise_huge(uint8_t *dst, size_t n) {
+    static const bool on = [] {
+        const char *e = getenv("RLNC_COPY_HUGEPAGE");
+        return !e || atoi(e) != 0;
+    }();
+    constexpr uintptr_t kHuge = uintptr_t(2) << 20;
+    const uintptr_t a = (reinterpret_cast<uintptr_t>(dst) + kHuge - 1) & ~(kHuge - 1);
+    const uintptr_t b = (reinterpret_cast<uintptr_t>(dst) + n) & ~(kHuge - 1);
+    if (on && b > a) (void)madvise(reinterpret_cast<void *>(a), b - a, MADV_HUGEPAGE);
+}
+
 int copy_out(CallWs *ws, uint8_t *dst, const uint8_t *src_dev, size_t n) {
     const int threads = copy_threads();
     if (n < kOutParallelMin || threads <= 1) {
@@ -995,6 +1035,7 @@ int copy_out(CallWs *ws, uint8_t *dst, const uint8_t *src_dev, size_t n) {
     for (hipEvent_t &e : ws->out_ev)
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     uint8_t *stage = ws->pin_out.as<uint8_t>();
+    advise_huge(dst, n);
     const size_t chunks = (n + kOutChunk - 1) / kOutChunk;
     auto issue = [&](size_t c) -> int {
         const size_t off = c * kOutChunk, len = std::min(kOutChunk, n - off);
@@ -1004,13 +1045,24 @@ int copy_out(CallWs *ws, uint8_t *dst, const uint8_t *src_dev, size_t n) {
     };
     for (size_t c = 0; c < std::min<size_t>(R, chunks); ++c)
         if (int st = issue(c)) return st;
+    const bool tr = g_copy_trace.on;
+    const uint64_t t0 = tr ? now_ns() : 0;
+    uint64_t tw = 0, tc = 0, tf = 0;
     for (size_t c = 0; c < chunks; ++c) {
+        const uint64_t a = tr ? now_ns() : 0;
         HIP_TRY(hipEventSynchronize(ws->out_ev[c % R]));
+        const uint64_t b = tr ? now_ns() : 0;
         const size_t off = c * kOutChunk, len = std::min(kOutChunk, n - off);
         par_copy(dst + off, stage + (c % R) * kOutChunk, len, threads);
+        if (tr) {
+            tw += b - a;
+            tc += now_ns() - b;
+            if (c == 0) tf = b - a;
+        }
         if (c + R < chunks)
             if (int st = issue(c + R)) return st;
     }
+    if (tr) g_copy_trace.add((now_ns() - t0) / 1e3f, tw / 1e3f, tc / 1e3f, tf / 1e3f);
     return RLNC_OK;
 }
 }  // namespace

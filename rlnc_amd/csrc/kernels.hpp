@@ -171,6 +171,8 @@ struct RrefParams {
     uint32_t *bsj_stream = nullptr;
     uint32_t bsj_block_bytes = 0;
     int bsj_tile_rows = 0;
+    // diagnostic build only (rref_ab.hip, RLNC_SMALL_PROF): per-wave phase timestamps of the small-object kernel
+    uint64_t *prof = nullptr;
 };
 // One object of a ragged elimination launch (rlnc_decode_ragged): T is k x m row-major, status m entries.
 struct RrefObj {

@@ -145,8 +145,10 @@ static hipError_t launch_rref_one(const RrefParams &p, hipStream_t s, bool *bsj_
         // rows of 8 dwords or fewer (k + m <= 32): 8 lane groups of 4 registers (123 VGPRs: 4 waves per SIMD) and
         // kSmallNW objects per workgroup; wider rows: 4 groups of 8 (199 VGPRs, 2 waves per SIMD, where the 8 objects
         // per CU the one-object workgroups already hold are all the VGPRs allow) -- profiles/r03_small_elim_ab.txt
+        // rows <= k <= 16 = G x RT: 2 registers of 8 lane groups (4 of 4 groups) hold every row; the round-4 forms
+        // carried 4 (8) registers per lane, half of them always zero rows (products with q = 0, still issued)
         const bool g8 = rref_row_dwords(p.k, p.m) <= 8;
-        auto kern = g8 ? &gf_rref_small_kernel<kSmallNW, 8, 4> : &gf_rref_small_kernel<1, 4, 8>;
+        auto kern = g8 ? &gf_rref_small_kernel<kSmallNW, 8, 2> : &gf_rref_small_kernel<1, 4, 4>;
         int nw = g8 ? kSmallNW : 1;
         const size_t lds_small = size_t(kTabEntries) * kTabDw * 4 + nw * rref_small_wave_bytes(p.k, p.m);
         hipLaunchKernelGGL(kern, dim3((p.n_obj + nw - 1) / nw), dim3(64 * nw), lds_small, s, p);

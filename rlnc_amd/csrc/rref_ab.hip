@@ -70,7 +70,7 @@ static hipError_t launch_rref_one_ab(const RrefParams &p, hipStream_t s) {
         // kSmallNW objects per workgroup; wider rows: 4 groups of 8 (199 VGPRs, 2 waves per SIMD, where the 8 objects
         // per CU the one-object workgroups already hold are all the VGPRs allow) -- profiles/r03_small_elim_ab.txt
         const bool g8 = rref_row_dwords(p.k, p.m) <= 8;
-        auto kern = g8 ? &gf_rref_small_kernel<kSmallNW, 8, 4> : &gf_rref_small_kernel<1, 4, 8>;
+        auto kern = g8 ? &gf_rref_small_kernel<kSmallNW, 8, 2> : &gf_rref_small_kernel<1, 4, 4>;
         int nw = g8 ? kSmallNW : 1;
         static const int nw_ab = [] {
             const char *e = getenv("RLNC_SMALL_NW");
@@ -79,11 +79,19 @@ static hipError_t launch_rref_one_ab(const RrefParams &p, hipStream_t s) {
         if (nw_ab == 1 || nw_ab == 2 || nw_ab == 8) {
             nw = nw_ab;
             if (g8)
-                kern = nw == 1 ? &gf_rref_small_kernel<1, 8, 4> : nw == 2 ? &gf_rref_small_kernel<2, 8, 4> : &gf_rref_small_kernel<8, 8, 4>;
+                kern = nw == 1 ? &gf_rref_small_kernel<1, 8, 2> : nw == 2 ? &gf_rref_small_kernel<2, 8, 2> : &gf_rref_small_kernel<8, 8, 2>;
             else
-                kern = nw == 1 ? &gf_rref_small_kernel<1, 4, 8> : nw == 2 ? &gf_rref_small_kernel<2, 4, 8> : &gf_rref_small_kernel<8, 4, 8>;
+                kern = nw == 1 ? &gf_rref_small_kernel<1, 4, 4> : nw == 2 ? &gf_rref_small_kernel<2, 4, 4> : &gf_rref_small_kernel<8, 4, 4>;
         }
         const size_t lds_small = size_t(kTabEntries) * kTabDw * 4 + nw * rref_small_wave_bytes(p.k, p.m);
+        if (const char *pe = getenv("RLNC_SMALL_PROF"); pe && g8 && nw == kSmallNW) {
+            // per-wave phase timestamps (8 x u64 per object) into the device buffer at this hex address
+            RrefParams q = p;
+            q.prof = reinterpret_cast<uint64_t *>(strtoull(pe, nullptr, 16));
+            hipLaunchKernelGGL((gf_rref_small_kernel<kSmallNW, 8, 2, true>), dim3((p.n_obj + nw - 1) / nw), dim3(64 * nw),
+                               lds_small, s, q);
+            return hipGetLastError();
+        }
         hipLaunchKernelGGL(kern, dim3((p.n_obj + nw - 1) / nw), dim3(64 * nw), lds_small, s, p);
         return hipGetLastError();
     }

@@ -861,11 +861,13 @@ __host__ __device__ inline size_t rref_small_wave_bytes(int k, int m) {
 constexpr int kSmallNW = 4;
 constexpr int kSmallMinObjects = 2048;
 
-template <int NW, int G, int RT>
+template <int NW, int G, int RT, bool PROF = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 ? 4 : 1))) void gf_rref_small_kernel(RrefParams p) {
     extern __shared__ uint32_t lds[];
     uint32_t *tab = lds;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    uint64_t ts[6] = {};  // PROF (diagnostic build): wave start, table copied, headers staged, pieces done, end
+    if constexpr (PROF) ts[0] = wall_clock64();
     {  // the shared table copy, all loads in flight at once
         constexpr int kPer = kTabEntries * kTabDw / 4 / (64 * NW);
         const uint4 *src = reinterpret_cast<const uint4 *>(kRrefTable.v);
@@ -877,6 +879,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 
         for (int u = 0; u < kPer; ++u) dst[tid + 64 * NW * u] = t4[u];
     }
     __syncthreads();  // the only workgroup barrier
+    if constexpr (PROF) ts[1] = wall_clock64();
     const int o = blockIdx.x * NW + wave;
     if (o >= p.n_obj) return;
     const int k = p.k, m = p.m;
@@ -901,6 +904,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 
     }
     for (int w = lane; w < (k + 1) * M.D; w += 64) M.w[w] = 0;
     rsync<false>();
+    if constexpr (PROF) ts[2] = wall_clock64();
 
     int rows = 0;
     bool clean = true;
@@ -929,6 +933,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 
     }
     if (clean) regs_to_lds<G, RT, false>(M, v, rows);
     rsync<false>();
+    if constexpr (PROF) ts[3] = wall_clock64();
     for (int pc = lane; pc < m; pc += 64) p.status[int64_t(o) * m + pc] = St[pc];
     if (lane == 0) p.rank[o] = rows;
     uint8_t *T = p.T + int64_t(o) * p.T_obj;
@@ -943,6 +948,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 
             const int s = e / tr, r = e % tr;
             st[e] = (r < rows ? uint32_t(M.b[r * M.S + k + s]) : 0u) * p.bsj_block_bytes;
         }
+    }
+    if constexpr (PROF) {
+        ts[4] = wall_clock64();
+        ts[5] = __smid();
+        if (lane < 6) p.prof[int64_t(o) * 8 + lane] = ts[lane];
     }
 }
 

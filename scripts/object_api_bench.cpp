@@ -2,8 +2,9 @@
 // × k = 16..256, recoders over k / 2 received pieces) on the drop-in object API (include/rlnc/full.hpp over
 // librlnc_hip), timed per call the way divan times it: one call per sample, inputs built outside the timed region,
 // the median over the samples.  A C++ caller, as a Rust caller of the crate would be: no interpreter between the
-// timer and the C ABI.  Beside each row: the reference's published EPYC 9R14 single-thread median (README.md:2859-2888
-// encode_zero_alloc, :3358-3387 recode_zero_alloc, :3736-3765 decode) and our/their ratio.
+// timer and the C ABI.  Beside each row: the reference's published EPYC 9R14 single-thread median (README.md:2738-2850
+// encode, :2859-2888 encode_zero_alloc, :3237-3349 recode, :3358-3387 recode_zero_alloc, :3736-3765 decode) and
+// our/their ratio: the reference's five benches x its 15 shapes.
 //
 // decode: the reference's region is the loop of Decoder::decode calls until ReceivedAllPieces (full_rlnc_decoder.rs:
 // 113-138: it never calls get_decoded_data).  Our decode() defers the data product to get_decoded_data, so each row
@@ -61,6 +62,12 @@ const Cfg kArgs[15] = {{1u << 20, 16}, {1u << 20, 32}, {1u << 20, 64}, {1u << 20
 // EPYC 9R14 medians, microseconds (README.md rows in kArgs order)
 const double kEncUs[15] = {22.3, 22.38, 19.58, 17.43, 17.47, 456, 414.4, 408.1, 405.3, 403.7,
                            1268, 1192, 1431, 1456, 1507};
+// the allocating forms, encode (full_rlnc_encoder.rs:103-117: Encoder::code returns a fresh Vec) and recode
+// (full_rlnc_recoder.rs:120-144: Recoder::recode), README.md:2738-2850 and :3237-3349
+const double kEncAllocUs[15] = {23.1, 25.13, 18.91, 20.15, 20.09, 464.6, 411.7, 434.2, 440.1, 436,
+                                1337, 1253, 1541, 1513, 1582};
+const double kRecAllocUs[15] = {13.95, 11.49, 11.24, 18.42, 48.8, 288.5, 273.9, 277.7, 274.1, 308.7,
+                                692.4, 636.3, 723.1, 821.8, 858.9};
 const double kRecUs[15] = {11.86, 12.33, 11.1, 18.15, 50.01, 218.5, 218.4, 211.2, 213.6, 234.2,
                            655.9, 641.9, 720.4, 811.5, 805.6};
 const double kDecUs[15] = {446, 834.3, 1681, 3850, 12700, 8655, 15410, 28740, 57290, 119300,
@@ -107,6 +114,29 @@ int main(int argc, char **argv) {
                         m / kEncUs[a]);
             std::fflush(stdout);
         }
+        // ---- encode (full_rlnc_encoder.rs:103-117): Encoder::code allocates the coded piece it returns; the returned
+        // pieces are dropped outside the timed region (divan drops bench outputs after timing)
+        if (!only || std::strcmp(only, "encode") == 0) {
+            for (int i = 0; i < 5; ++i) (void)enc.code(rng);
+            const int n = samples_for(kEncAllocUs[a], quick);
+            std::vector<double> t;
+            for (int i = 0; i < n; ++i) {
+                double t1;
+                {
+                    const double t0 = now_us();
+                    const std::vector<uint8_t> piece = enc.code(rng);
+                    t1 = now_us();
+                    t.push_back(t1 - t0);
+                }  // dropped after the timer, as divan drops a sample's output
+            }
+            const double m = median(t), counter = double(c.k * L + full);
+            std::printf("{\"bench\": \"encode\", \"data_bytes\": %zu, \"k\": %zu, \"L\": %zu, \"samples\": %d, "
+                        "\"median_us\": %.2f, \"GiBps\": %.2f, \"epyc_median_us\": %.2f, \"epyc_GiBps\": %.2f, "
+                        "\"time_vs_epyc\": %.3f}\n",
+                        c.bytes, c.k, L, n, m, counter / m * 1e6 / kGiB, kEncAllocUs[a],
+                        counter / kEncAllocUs[a] * 1e6 / kGiB, m / kEncAllocUs[a]);
+            std::fflush(stdout);
+        }
         // ---- recode_zero_alloc (full_rlnc_recoder.rs:148-173): a fresh Recoder over k/2 coded pieces per sample
         if (!only || std::strcmp(only, "recode") == 0) {
             const size_t nrec = c.k / 2;
@@ -135,6 +165,21 @@ int main(int argc, char **argv) {
                         "\"epyc_GiBps\": %.2f, \"time_vs_epyc\": %.3f}\n",
                         c.bytes, c.k, nrec, n, m, counter / m * 1e6 / kGiB, kRecUs[a], counter / kRecUs[a] * 1e6 / kGiB,
                         m / kRecUs[a]);
+            std::fflush(stdout);
+            // ---- recode (full_rlnc_recoder.rs:120-144): Recoder::recode allocates the recoded piece it returns
+            std::vector<double> ta;
+            for (int i = 0; i < n; ++i) {
+                Recoder r = Recoder::create(coded, full, c.k).unwrap();
+                const double t0 = now_us();
+                const std::vector<uint8_t> piece = r.recode(rng);
+                ta.push_back(now_us() - t0);
+            }
+            const double ma = median(ta);
+            std::printf("{\"bench\": \"recode\", \"data_bytes\": %zu, \"k\": %zu, \"received\": %zu, "
+                        "\"samples\": %d, \"median_us\": %.2f, \"GiBps\": %.2f, \"epyc_median_us\": %.2f, "
+                        "\"epyc_GiBps\": %.2f, \"time_vs_epyc\": %.3f}\n",
+                        c.bytes, c.k, nrec, n, ma, counter / ma * 1e6 / kGiB, kRecAllocUs[a],
+                        counter / kRecAllocUs[a] * 1e6 / kGiB, ma / kRecAllocUs[a]);
             std::fflush(stdout);
         }
         // ---- decode (full_rlnc_decoder.rs:106-139): 2k coded pieces, a fresh Decoder per sample

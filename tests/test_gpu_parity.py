@@ -791,11 +791,13 @@ def test_large_piece_count_recode(ctx, orc, k, n, count):
 
 
 @pytest.mark.parametrize("k,m,sparsity,dep,nobj", [(16, 16, 0.0, 0.0, 2048), (16, 24, 0.5, 0.1, 2051),
-                                                  (8, 12, 0.7, 0.1, 2049)])
+                                                  (8, 12, 0.7, 0.1, 2049), (16, 16, 0.3, 0.1, 6001),
+                                                  (12, 20, 0.6, 0.2, 5000)])
 def test_decode_many_small_objects(ctx, k, m, sparsity, dep, nobj):
     """>= 2,048 objects with k <= 16: the default path takes the multi-object kernel (rref.hip gf_rref_small_kernel,
     4 objects per workgroup: 2,049 and 2,051 leave the last workgroup part-empty; rows of <= 8 dwords on 8 lane
-    groups, else 4); every object's statuses and payload rows against the oracle."""
+    groups, else 4; 5,000 and 6,001 objects: more than one round of waves); every object's statuses and payload rows
+    against the oracle."""
     from rlnc_amd import batch
 
     rng = np.random.default_rng(2048 + k * 3 + m)
@@ -922,3 +924,4 @@ def test_encode_plan_written_ahead(orc, variant, k, L, n):
         batch.encode_batch_data_planned(src, other, pieces, plan, c1)
     c1.close()
     c2.close()
+
