@@ -1011,58 +1011,84 @@ hipError_t launch_vec(uint8_t *dst, const uint8_t *src, int64_t len, uint8_t c, 
 // get_final_data_len on device (decoder.rs:162-177).  Equivalent formulation: the last nonzero byte of
 // the padded payload must be the boundary marker and must not sit at index 0.
 // ---------------------------------------------------------------------------------------------------
-// One wave per object scans 1 KiB chunks from the END of the payload: for any padded object the last
+// 16 lanes per object (one DPP row, 64 B a lane) scan 1 KiB chunks from the END of the payload: for any padded object the last
 // nonzero byte lies in the final k bytes (Encoder::new pads with < k zeros after the marker,
 // encoder.rs:95-99), so the scan normally stops after one chunk — O(1) instead of a full re-read.  The same wave
 // then checks the marker and writes the object's status and length (one launch; the round-3 form wrote the index
 // to scratch for a second kernel: 5.5 us more per decode of configs[0]'s 4,096 objects).
-// rank != nullptr: objects of rank < k are NotAllPiecesReceivedYet (decoder.rs:137-139) and not scanned;
-// invalid_code: the status of a payload without a valid marker.
+// rank != nullptr: objects of rank < k are NotAllPiecesReceivedYet (decoder.rs:137-139); the rank is loaded beside
+// the first chunk (their latencies overlap) and decides the outcome; invalid_code: the status of a payload without a
+// valid marker.  The row maximum is a DPP ladder (row16_max), not __shfl_xor; 16 objects per workgroup: a quarter of
+// the waves of the round-4 one-wave-per-object form.
+// max over one 16-lane DPP row of a 32-bit key (every lane of the row ends with it): VALU row rotations only
+__device__ __forceinline__ uint32_t row16_max(uint32_t a) {
+    a = max(a, uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x121, 0xf, 0xf, false)));  // row_ror:1
+    a = max(a, uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x122, 0xf, 0xf, false)));  // row_ror:2
+    a = max(a, uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x124, 0xf, 0xf, false)));  // row_ror:4
+    a = max(a, uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x128, 0xf, 0xf, false)));  // row_ror:8
+    return a;
+}
+
+constexpr int kScanObjPerWg = 16;  // 16 lanes (one DPP row) per object, 16 objects per 256-thread workgroup
+
 template <bool ALIGNED>
-__global__ __launch_bounds__(64) void final_len_scan_kernel(const uint8_t *data, int64_t obj_stride, int64_t len,
-                                                            const int32_t *rank, int k, int32_t *status,
-                                                            int64_t *final_len, int32_t invalid_code) {
-    const int obj = blockIdx.x;
-    const int lane = threadIdx.x;
-    if (rank != nullptr && rank[obj] < k) {  // not decoded: NotAllPiecesReceivedYet, no data to scan
-        if (lane == 0) {
+__global__ __launch_bounds__(256) void final_len_scan_kernel(const uint8_t *data, int64_t obj_stride, int64_t len,
+                                                             int n_obj, const int32_t *rank, int k, int32_t *status,
+                                                             int64_t *final_len, int32_t invalid_code) {
+    const int tid = threadIdx.x, l = tid & 15;
+    const int obj = blockIdx.x * kScanObjPerWg + (tid >> 4);
+    const bool valid = obj < n_obj;
+    const int32_t rk = (valid && rank != nullptr) ? rank[obj] : k;
+    const uint8_t *d = data + int64_t(valid ? obj : 0) * obj_stride;
+    int64_t c = (len + 1023) / 1024 - 1;  // this object's chunk, from the end
+    bool done = !valid;
+    int64_t hit = -1;  // index of the payload's last nonzero byte
+    uint32_t byte = 0;
+    for (;;) {
+        // (index in the chunk + 1) << 8 | byte of the last nonzero byte of this lane's 64 B, 0 = none: the maximum
+        // over the object's 16 lanes is the chunk's last nonzero byte with its value
+        uint32_t mine = 0;
+        if (!done) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t off = c * 1024 + l * 64 + u * kBytesPerThread;
+                if (off < len) {
+                    const int nb = int(min<int64_t>(kBytesPerThread, len - off));
+                    const uint4 x = load16<ALIGNED>(d + off, nb);
+                    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (w[q]) {
+                            const int b = (31 - __builtin_clz(w[q])) / 8;
+                            mine = (uint32_t(l * 64 + u * kBytesPerThread + 4 * q + b + 1) << 8) |
+                                   ((w[q] >> (8 * b)) & 0xFFu);
+                        }
+                }
+            }
+        }
+        const uint32_t best = row16_max(mine);
+        if (!done) {
+            if (best) {
+                hit = c * 1024 + int64_t(best >> 8) - 1;
+                byte = best & 0xFFu;
+                done = true;
+            } else if (rk < k || c == 0) {
+                done = true;  // not decoded (nothing to scan), or an all-zero payload
+            } else {
+                --c;
+            }
+        }
+        if (__ballot(!done) == 0) break;
+    }
+    if (valid && l == 0) {
+        if (rk < k) {
             status[obj] = RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;
             final_len[obj] = 0;
+        } else {
+            const bool ok = hit > 0 && byte == kBoundaryMarker;  // decoder.rs:162-177
+            status[obj] = ok ? RLNC_OK : invalid_code;
+            final_len[obj] = ok ? hit : 0;
         }
-        return;
-    }
-    const uint8_t *d = data + int64_t(obj) * obj_stride;
-    // (index + 1) << 8 | byte of the last nonzero byte in this lane's 16 B, 0 = none: the maximum over the wave is
-    // the payload's last nonzero byte with its value
-    unsigned long long best = 0;
-    for (int64_t c = (len + 1023) / 1024 - 1; c >= 0; --c) {
-        const int64_t off = c * 1024 + int64_t(lane) * kBytesPerThread;
-        unsigned long long mine = 0;
-        if (off < len) {
-            const int nb = int(min<int64_t>(kBytesPerThread, len - off));
-            const uint4 x = load16<ALIGNED>(d + off, nb);
-            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (w[q]) {
-                    const int b = (31 - __builtin_clz(w[q])) / 8;
-                    mine = ((unsigned long long)(off + 4 * q + b + 1) << 8) | ((w[q] >> (8 * b)) & 0xFFu);
-                }
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long v = __shfl_xor(mine, o);
-            mine = v > mine ? v : mine;
-        }
-        if (mine) {  // wave-uniform after the reduction
-            best = mine;
-            break;
-        }
-    }
-    if (lane == 0) {
-        const int64_t idx = int64_t(best >> 8) - 1;
-        const bool ok = best != 0 && idx != 0 && (best & 0xFFu) == kBoundaryMarker;  // decoder.rs:162-177
-        status[obj] = ok ? RLNC_OK : invalid_code;
-        final_len[obj] = ok ? idx : 0;
     }
 }
 
@@ -1082,11 +1108,13 @@ hipError_t launch_final_data_len_ranked(const uint8_t *data, int64_t obj_stride,
                                         const int32_t *rank, int32_t *status, int64_t *final_len, hipStream_t s) {
     if (n_obj <= 0) return hipSuccess;
     if (unaligned_vector_ok() || (al16(data) && (n_obj == 1 || al16(obj_stride))))
-        hipLaunchKernelGGL(final_len_scan_kernel<true>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, rank, k,
-                           status, final_len, int32_t(RLNC_ERR_INVALID_DECODED_DATA_FORMAT));
+        hipLaunchKernelGGL(final_len_scan_kernel<true>, dim3((n_obj + kScanObjPerWg - 1) / kScanObjPerWg), dim3(256), 0,
+                           s, data, obj_stride, len, n_obj, rank, k, status, final_len,
+                           int32_t(RLNC_ERR_INVALID_DECODED_DATA_FORMAT));
     else
-        hipLaunchKernelGGL(final_len_scan_kernel<false>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, rank, k,
-                           status, final_len, int32_t(RLNC_ERR_INVALID_DECODED_DATA_FORMAT));
+        hipLaunchKernelGGL(final_len_scan_kernel<false>, dim3((n_obj + kScanObjPerWg - 1) / kScanObjPerWg), dim3(256), 0,
+                           s, data, obj_stride, len, n_obj, rank, k, status, final_len,
+                           int32_t(RLNC_ERR_INVALID_DECODED_DATA_FORMAT));
     return hipGetLastError();
 }
 
@@ -1506,11 +1534,11 @@ hipError_t launch_final_data_len(const uint8_t *data, int64_t obj_stride, int64_
                                  int64_t *final_len, int32_t invalid_code, hipStream_t s) {
     if (n_obj <= 0) return hipSuccess;
     if (unaligned_vector_ok() || (al16(data) && (n_obj == 1 || al16(obj_stride))))
-        hipLaunchKernelGGL(final_len_scan_kernel<true>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, nullptr, 0,
-                           status, final_len, invalid_code);
+        hipLaunchKernelGGL(final_len_scan_kernel<true>, dim3((n_obj + kScanObjPerWg - 1) / kScanObjPerWg), dim3(256), 0,
+                           s, data, obj_stride, len, n_obj, nullptr, 0, status, final_len, invalid_code);
     else
-        hipLaunchKernelGGL(final_len_scan_kernel<false>, dim3(n_obj), dim3(64), 0, s, data, obj_stride, len, nullptr,
-                           0, status, final_len, invalid_code);
+        hipLaunchKernelGGL(final_len_scan_kernel<false>, dim3((n_obj + kScanObjPerWg - 1) / kScanObjPerWg), dim3(256), 0,
+                           s, data, obj_stride, len, n_obj, nullptr, 0, status, final_len, invalid_code);
     return hipGetLastError();
 }
 

@@ -477,15 +477,23 @@ __device__ __forceinline__ void load_fwd(const Mat &M, const uint32_t *tab, cons
         const uint32_t x = h[i < k ? i : k - 1];
         f.q[t] = i < r ? x : 0u;
     }
+    // this lane's dword of [coeffs | unit vector of slot pc]: with k a multiple of 4 the coefficient dwords are whole
+    // dwords of the staged header (4-byte aligned: H is, and pc·k is) -- one clamped load and selects, no per-byte
+    // divergent reads (k is uniform: the branch is too)
     uint32_t init = 0;
-    if (w < M.D) {
+    const int c0 = 4 * w;
+    if ((k & 3) == 0) {
+        const uint32_t x = reinterpret_cast<const uint32_t *>(h)[min(w, (k >> 2) - 1)];
+        init = c0 < k ? x : 0u;
+    } else if (w < M.D) {
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            const int c = 4 * w + b;
-            const uint32_t x = c < k ? uint32_t(h[c]) : uint32_t(c == k + pc);
-            init |= x << (8 * b);
+            const int c = c0 + b;
+            init |= (c < k ? uint32_t(h[c < k ? c : 0]) : 0u) << (8 * b);
         }
     }
+    const int u = k + pc - c0;  // the unit vector's byte in this dword
+    if (w < M.D && u >= 0 && u < 4) init |= 1u << (8 * u);
     f.init = init;
     if constexpr (FwdOps<G, RT>::kPre) {
 #pragma unroll
@@ -518,6 +526,11 @@ __device__ __forceinline__ uint32_t dot_chunked(const uint32_t *tab, const uint3
 // Runs pieces pc, pc+1, ... on the registers while the matrix stays a clean RREF (the next piece's forward
 // operands are loaded while the current one finishes).  Returns the next piece index; on leaving the clean
 // state (a kept row with a zero diagonal) the whole matrix is written back to LDS and *clean = false.
+#ifndef RLNC_SMALL_PRIO
+#define RLNC_SMALL_PRIO 1
+#endif
+constexpr bool kSmallPrio = RLNC_SMALL_PRIO != 0;
+
 template <int G, int RT, bool WG = true>
 __device__ int reg_run(const Mat &M, const uint32_t *tab, uint32_t (&v)[RT], const uint8_t *H, int pc, int m, int k,
                        int &rows, bool &clean, int32_t *St) {
@@ -528,9 +541,23 @@ __device__ int reg_run(const Mat &M, const uint32_t *tab, uint32_t (&v)[RT], con
     uint32_t cm = 0;  // coefficient bytes (< k) of this lane's dword
     if (wl && 4 * w < k) cm = 4 * w + 4 <= k ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (8 * (4 * w + 4 - k)));
     FwdOps<G, RT> f;
+    pc = __builtin_amdgcn_readfirstlane(pc);  // uniform piece index: scalar loop control
     load_fwd<G, RT>(M, tab, H, pc, rows, k, f);
     for (; pc < m; ++pc) {
-        const int r = rows;
+        if constexpr (!WG) {
+            // one wave per object, several objects per SIMD (the small-object kernel): a wave that has fallen behind
+            // wins issue over one ahead of it -- priority 3 for the first quarter of the pieces down to 0 for the last
+            // -- so the SIMD's objects finish together instead of one straggler setting the kernel's end
+            // (RLNC_SMALL_PRIO diagnostic knob: the A/B build compiles both)
+            if (kSmallPrio) {  // s_setprio takes an immediate: step down at the quarter marks
+                const int q4 = 4 * pc;
+                if (q4 < m) __builtin_amdgcn_s_setprio(3);
+                else if (q4 < 2 * m) __builtin_amdgcn_s_setprio(2);
+                else if (q4 < 3 * m) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+        }
+        const int r = __builtin_amdgcn_readfirstlane(rows);  // uniform: scalar branches and shift amounts below
         if (r == k) {  // decoder.rs:97-99
             if (lane == 0) St[pc] = RLNC_ERR_RECEIVED_ALL_PIECES;
             continue;
@@ -546,7 +573,7 @@ __device__ int reg_run(const Mat &M, const uint32_t *tab, uint32_t (&v)[RT], con
         acc = group_xor<DP>(acc);
         uint32_t nr = f.init ^ acc;
         const int rw = r >> 2, rb = 8 * (r & 3);
-        const uint32_t piv = (__builtin_amdgcn_readlane(nr, rw) >> rb) & 0xFFu;
+        const uint32_t piv = __builtin_amdgcn_readfirstlane((__builtin_amdgcn_readlane(nr, rw) >> rb) & 0xFFu);
         if (piv == 0) {
             const bool keep = ballot((nr & cm) != 0) != 0;  // remove_zero_rows (:222-244)
             if (lane == 0) St[pc] = keep ? RLNC_OK : RLNC_ERR_PIECE_NOT_USEFUL;
@@ -668,7 +695,7 @@ __device__ int reg_run_mw(const Mat &M, const uint32_t *tab, const uint8_t *H, u
         for (int s = 0; s < NW; ++s) nr ^= Pb[s * DP + w];
         buf ^= 1;
         const int rw = r >> 2, rb = 8 * (r & 3);
-        const uint32_t piv = (__builtin_amdgcn_readlane(nr, rw) >> rb) & 0xFFu;
+        const uint32_t piv = __builtin_amdgcn_readfirstlane((__builtin_amdgcn_readlane(nr, rw) >> rb) & 0xFFu);
         if (piv == 0) {
             const bool keep = ballot((nr & cm) != 0) != 0;  // remove_zero_rows (:222-244)
             if (threadIdx.x == 0) St[pc] = keep ? RLNC_OK : RLNC_ERR_PIECE_NOT_USEFUL;
@@ -861,101 +888,6 @@ __host__ __device__ inline size_t rref_small_wave_bytes(int k, int m) {
 constexpr int kSmallNW = 4;
 constexpr int kSmallMinObjects = 2048;
 
-template <int NW, int G, int RT, bool PROF = false>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 ? 4 : 1))) void gf_rref_small_kernel(RrefParams p) {
-    extern __shared__ uint32_t lds[];
-    uint32_t *tab = lds;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    uint64_t ts[6] = {};  // PROF (diagnostic build): wave start, table copied, headers staged, pieces done, end
-    if constexpr (PROF) ts[0] = wall_clock64();
-    {  // the shared table copy, all loads in flight at once
-        constexpr int kPer = kTabEntries * kTabDw / 4 / (64 * NW);
-        const uint4 *src = reinterpret_cast<const uint4 *>(kRrefTable.v);
-        uint4 *dst = reinterpret_cast<uint4 *>(tab);
-        uint4 t4[kPer];
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) t4[u] = src[tid + 64 * NW * u];
-#pragma unroll
-        for (int u = 0; u < kPer; ++u) dst[tid + 64 * NW * u] = t4[u];
-    }
-    __syncthreads();  // the only workgroup barrier
-    if constexpr (PROF) ts[1] = wall_clock64();
-    const int o = blockIdx.x * NW + wave;
-    if (o >= p.n_obj) return;
-    const int k = p.k, m = p.m;
-    Mat M;
-    M.D = rref_row_dwords(k, m);
-    M.S = 4 * M.D;
-    M.w = lds + kTabEntries * kTabDw + size_t(wave) * (rref_small_wave_bytes(k, m) / 4);
-    M.b = reinterpret_cast<uint8_t *>(M.w);
-    int32_t *St = reinterpret_cast<int32_t *>(M.b + size_t(k + 1) * M.S);
-    uint8_t *H = reinterpret_cast<uint8_t *>(St + ((m + 3) & ~3));
-    const uint8_t *base = p.pieces + int64_t(o) * p.obj_stride;
-    for (int e0 = 0; e0 < m * k; e0 += 64 * 16) {  // staged headers, 16 byte loads in flight per lane
-        uint8_t hb[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int e = e0 + lane + 64 * u;
-            hb[u] = e < m * k ? base[int64_t(e / k) * p.piece_stride + e % k] : uint8_t(0);
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-            if (e0 + lane + 64 * u < m * k) H[e0 + lane + 64 * u] = hb[u];
-    }
-    for (int w = lane; w < (k + 1) * M.D; w += 64) M.w[w] = 0;
-    rsync<false>();
-    if constexpr (PROF) ts[2] = wall_clock64();
-
-    int rows = 0;
-    bool clean = true;
-    uint32_t v[RT];
-#pragma unroll
-    for (int t = 0; t < RT; ++t) v[t] = 0;
-    for (int pc = 0; pc < m; ++pc) {
-        if (clean) {
-            pc = reg_run<G, RT, false>(M, tab, v, H, pc, m, k, rows, clean, St);
-            rsync<false>();
-            if (pc >= m) break;
-        }
-        if (rows == k) {  // decoder.rs:97-99
-            if (lane == 0) St[pc] = RLNC_ERR_RECEIVED_ALL_PIECES;
-            continue;
-        }
-        // add_row (decoder_matrix.rs:53-62), then the reference's rref verbatim (decoder_matrix.rs:99-244)
-        for (int c = lane; c < M.S; c += 64) M.b[rows * M.S + c] = c < k ? H[pc * k + c] : uint8_t(c == k + pc);
-        rsync<false>();
-        const int before = rows;
-        rows = generic_rref<false>(M, tab, rows + 1, k);
-        clean = is_clean(M, rows);
-        if (clean) lds_to_regs<G, RT>(M, v, rows);
-        if (lane == 0) St[pc] = rows == before ? RLNC_ERR_PIECE_NOT_USEFUL : RLNC_OK;  // decoder.rs:112-117
-        rsync<false>();
-    }
-    if (clean) regs_to_lds<G, RT, false>(M, v, rows);
-    rsync<false>();
-    if constexpr (PROF) ts[3] = wall_clock64();
-    for (int pc = lane; pc < m; pc += 64) p.status[int64_t(o) * m + pc] = St[pc];
-    if (lane == 0) p.rank[o] = rows;
-    uint8_t *T = p.T + int64_t(o) * p.T_obj;
-    for (int e = lane; e < k * m; e += 64) {
-        const int r = e / m, s = e % m;
-        T[e] = r < rows ? M.b[r * M.S + k + s] : uint8_t(0);
-    }
-    if (p.bsj_stream != nullptr) {  // T again, as the product's block-offset stream ([j][i], i < tile rows)
-        const int tr = p.bsj_tile_rows;
-        uint32_t *st = p.bsj_stream + int64_t(o) * m * tr;
-        for (int e = lane; e < m * tr; e += 64) {
-            const int s = e / tr, r = e % tr;
-            st[e] = (r < rows ? uint32_t(M.b[r * M.S + k + s]) : 0u) * p.bsj_block_bytes;
-        }
-    }
-    if constexpr (PROF) {
-        ts[4] = wall_clock64();
-        ts[5] = __smid();
-        if (lane < 6) p.prof[int64_t(o) * 8 + lane] = ts[lane];
-    }
-}
-
 // ---------------------------------------------------------------------------------------------------
 // Blocked clean run (path 5, default when k + m <= 256): while rows 0..r-1 are a clean RREF, the next b <= B
 // pieces are appended in one block instead of one at a time:
@@ -1074,6 +1006,155 @@ __device__ int extend_prefix(const Mat &M, int cp, int R) {
         ++cp;
     }
     return cp;
+}
+
+// One piece outside the clean state, in one wave (the small-object kernel): rows 0..cp-1 are a clean prefix (M[i][i] = 1,
+// column i zero in every other prefix row), rows cp..rows-1 dirty; the piece's header becomes row `rows`.  The
+// reference's rref on such a matrix splits around the prefix exactly as gf_rref_block_kernel's dirty step relies on
+// (comment above forward_range): forward steps i < cp reduce each dirty row by its ORIGINAL byte i times prefix row i,
+// forward steps i >= cp run verbatim on the dirty rows, backward steps i >= cp eliminate column i from every row above
+// (prefix rows included) and normalise row i, backward steps i < cp change nothing, remove_zero_rows can only drop
+// dirty rows.  The generic path it replaces replayed every step of the whole matrix (~7 us a piece on a k = 16
+// object, 8x a clean piece: the kernel's tail, profiles/r05_small_elim_timeline.jsonl).  Updates rows and cp.
+__device__ void small_dirty_step(const Mat &M, const uint32_t *tab, const uint8_t *hdr, int pc, int k, int &rows,
+                                 int &cp) {
+    const int lane = lane_id();
+    const int D = M.D, G = 64 / D, w = lane % D, g = lane / D;
+    const int r0 = cp, R = rows;
+    for (int c = lane; c < M.S; c += 64) M.b[R * M.S + c] = c < k ? hdr[c] : uint8_t(c == k + pc);
+    rsync<false>();
+    // forward steps i < r0: dirty row t ^= Σ_{i<r0} M[t][i]·row_i, lane group g over prefix rows i ≡ g (mod G),
+    // the G partial sums met by group_xor; each row's quotients are read before its one write
+    if (r0 > 0) {
+        for (int t = r0; t <= R; ++t) {
+            uint32_t acc = 0;
+            for (int i = g; i < r0; i += G) acc ^= mul4(tab, M.at(t, i), M.w[i * D + w]);
+            acc = group_xor_rt(acc, D);
+            if (g == 0) M.w[t * D + w] ^= acc;
+        }
+        rsync<false>();
+    }
+    forward_range(M, tab, r0, R + 1);  // forward steps i >= r0, verbatim on the dirty rows
+    // backward steps i = R .. r0 (:171-215): column i out of every row above, then row i normalised from column i+1
+    for (int i = R; i >= r0; --i) {
+        const uint32_t piv = M.at(i, i);
+        if (piv == 0) continue;
+        const uint32_t xi = M.w[i * D + w];
+        const uint32_t nr = mul4(tab, 256 + piv, xi);  // row i · piv^-1: (q·piv^-1)·x = q·(piv^-1·x)
+        const uint32_t mi = from_mask(w, i);
+        for (int j = g; j < i; j += G) {
+            const uint32_t q = M.at(j, i);  // read by the whole wave before any lane rewrites row j
+            if (q) M.w[j * D + w] ^= mul4(tab, q, nr) & mi;
+        }
+        rsync<false>();
+        if (piv != 1) {
+            if (g == 0) {
+                const uint32_t mask = from_mask(w, i + 1);
+                uint32_t v = (xi & ~mask) | (nr & mask);
+                if (w == (i >> 2)) v = (v & ~(0xFFu << (8 * (i & 3)))) | (1u << (8 * (i & 3)));
+                M.w[i * D + w] = v;
+            }
+            rsync<false>();
+        }
+    }
+    rows = remove_zero_range(M, r0, R + 1, k);
+    cp = extend_prefix(M, r0, rows);
+}
+
+template <int NW, int G, int RT, bool PROF = false>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 ? 4 : 1))) void gf_rref_small_kernel(RrefParams p) {
+    extern __shared__ uint32_t lds[];
+    uint32_t *tab = lds;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    uint64_t ts[6] = {};  // PROF (diagnostic build): wave start, table copied, headers staged, pieces done, end
+    if constexpr (PROF) ts[0] = wall_clock64();
+    const int o = blockIdx.x * NW + wave;
+    const int k = p.k, m = p.m;  // k <= 16 and k + m <= 64 on this path (rref.hip small_many)
+    // this object's headers first (lane = piece, its k <= 16 coefficient bytes in flight at once, no index
+    // division), then the shared table copy: both global-load latencies overlap
+    uint8_t hb[16];
+    const bool hl = o < p.n_obj && lane < m;
+    const uint8_t *hp = p.pieces + int64_t(o) * p.obj_stride + int64_t(lane) * p.piece_stride;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) hb[u] = (hl && u < k) ? hp[u] : uint8_t(0);
+    {  // the shared table copy, all loads in flight at once
+        constexpr int kPer = kTabEntries * kTabDw / 4 / (64 * NW);
+        const uint4 *src = reinterpret_cast<const uint4 *>(kRrefTable.v);
+        uint4 *dst = reinterpret_cast<uint4 *>(tab);
+        uint4 t4[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) t4[u] = src[tid + 64 * NW * u];
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) dst[tid + 64 * NW * u] = t4[u];
+    }
+    Mat M;
+    M.D = rref_row_dwords(k, m);
+    M.S = 4 * M.D;
+    M.w = lds + kTabEntries * kTabDw + size_t(wave) * (rref_small_wave_bytes(k, m) / 4);
+    M.b = reinterpret_cast<uint8_t *>(M.w);
+    int32_t *St = reinterpret_cast<int32_t *>(M.b + size_t(k + 1) * M.S);
+    uint8_t *H = reinterpret_cast<uint8_t *>(St + ((m + 3) & ~3));
+    if (hl) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            if (u < k) H[lane * k + u] = hb[u];
+    }
+    for (int w = lane; w < (k + 1) * M.D; w += 64) M.w[w] = 0;
+    __syncthreads();  // the only workgroup barrier: the table, and this wave's headers and zeroed matrix
+    if constexpr (PROF) ts[1] = ts[2] = wall_clock64();
+    if (o >= p.n_obj) return;
+
+    int rows = 0, cp = -1;  // cp: the clean prefix while outside the clean state (-1 inside it)
+    bool clean = true;
+    uint32_t v[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) v[t] = 0;
+    for (int pc = 0; pc < m; ++pc) {
+        if (clean) {
+            pc = reg_run<G, RT, false>(M, tab, v, H, pc, m, k, rows, clean, St);
+            rsync<false>();
+            if (pc >= m) break;
+        }
+        if (rows == k) {  // decoder.rs:97-99
+            if (lane == 0) St[pc] = RLNC_ERR_RECEIVED_ALL_PIECES;
+            continue;
+        }
+        // add_row (decoder_matrix.rs:53-62) and the reference's rref (decoder_matrix.rs:99-244) on a clean prefix
+        // (rows < cp) + dirty rows, decomposed around the prefix (small_dirty_step)
+        if (cp < 0) cp = rows - 1;  // reg_run left the clean state: its last kept row is the first dirty one
+        const int before = rows;
+        if constexpr (PROF) ++ts[5];  // pieces outside the clean state
+        small_dirty_step(M, tab, H + pc * k, pc, k, rows, cp);
+        clean = cp == rows;
+        if (clean) {
+            lds_to_regs<G, RT>(M, v, rows);
+            cp = -1;
+        }
+        if (lane == 0) St[pc] = rows == before ? RLNC_ERR_PIECE_NOT_USEFUL : RLNC_OK;  // decoder.rs:112-117
+        rsync<false>();
+    }
+    if (clean) regs_to_lds<G, RT, false>(M, v, rows);
+    rsync<false>();
+    if constexpr (PROF) ts[3] = wall_clock64();
+    for (int pc = lane; pc < m; pc += 64) p.status[int64_t(o) * m + pc] = St[pc];
+    if (lane == 0) p.rank[o] = rows;
+    // T row by row, lane = column (m <= 64 here): no per-element index division
+    uint8_t *T = p.T + int64_t(o) * p.T_obj;
+    for (int r = 0; r < k; ++r)
+        if (lane < m) T[r * m + lane] = r < rows ? M.b[r * M.S + k + lane] : uint8_t(0);
+    if (p.bsj_stream != nullptr) {  // T again, as the product's block-offset stream ([j][i], i < tile rows)
+        const int tr = p.bsj_tile_rows;  // 8 or 16 (the 1- / 2-wave programs): lane = (column group, row)
+        uint32_t *st = p.bsj_stream + int64_t(o) * m * tr;
+        const int r = lane & (tr - 1), step = 64 / tr;
+        for (int s = lane / tr; s < m; s += step)
+            st[s * tr + r] = (r < rows ? uint32_t(M.b[r * M.S + k + s]) : 0u) * p.bsj_block_bytes;
+    }
+    if constexpr (PROF) {
+        ts[4] = wall_clock64();
+        ts[5] |= uint64_t(__smid()) << 32;
+        if (lane < 6) p.prof[int64_t(o) * 8 + lane] = ts[lane];
+        if (lane == 6) p.prof[int64_t(o) * 8 + 6] = uint64_t(rows);
+    }
 }
 
 struct Sel1 {  // v_perm selectors of one dword: bits 0-2, 3-5, 6-7 of every byte

@@ -49,11 +49,29 @@ def main():
            "start_us": pct(us[:, 0]), "end_us": pct(us[:, 4]),
            "table_copy_us": pct(us[:, 1] - us[:, 0]), "headers_us": pct(us[:, 2] - us[:, 1]),
            "pieces_us": pct(us[:, 3] - us[:, 2]), "outputs_us": pct(us[:, 4] - us[:, 3]),
-           "wave_life_us": pct(us[:, 4] - us[:, 0]), "distinct_cu_ids": int(len(np.unique(P[:, 5])))}
+           "wave_life_us": pct(us[:, 4] - us[:, 0]),
+           "distinct_cu_ids": int(len(np.unique(prof.cpu().numpy()[:, 5] >> 32)))}
+    dirty = (prof.cpu().numpy()[:, 5] & 0xFFFFFFFF).astype(np.int64)
+    rows = prof.cpu().numpy()[:, 6]
+    life = us[:, 4] - us[:, 0]
+    out["objects_with_dirty_pieces"] = int((dirty > 0).sum())
+    out["dirty_pieces_total"] = int(dirty.sum())
+    out["life_us_clean_objects"] = pct(life[dirty == 0]) if (dirty == 0).any() else None
+    out["life_us_dirty_objects"] = pct(life[dirty > 0]) if (dirty > 0).any() else None
+    out["rank_deficient_objects"] = int((rows < k).sum())
+    cu = (prof.cpu().numpy()[:, 5] >> 32).astype(np.int64)
+    ids, counts = np.unique(cu, return_counts=True)
+    out["objects_per_cu_hist"] = {int(c): int(n) for c, n in zip(*np.unique(counts, return_counts=True))}
+    per_cu = dict(zip(ids.tolist(), counts.tolist()))
+    by_count = {}
+    for i in range(B):
+        by_count.setdefault(per_cu[int(cu[i])], []).append(life[i])
+    out["life_us_median_by_cu_load"] = {int(c): round(float(np.median(v)), 2) for c, v in sorted(by_count.items())}
+    # the slowest 20 objects: (life us, dirty pieces, rows, cu)
+    idx = np.argsort(-life)[:20]
+    out["slowest"] = [[round(float(life[i]), 2), int(dirty[i]), int(rows[i]), int(prof.cpu().numpy()[i, 5] >> 32)]
+                      for i in idx]
     print(json.dumps(out), flush=True)
-    # start-time histogram: waves started per 2 us bin
-    h, e = np.histogram(us[:, 0], bins=np.arange(0, us[:, 4].max() + 2, 2))
-    print(json.dumps({"start_hist_2us": h.tolist()}), flush=True)
 
 
 if __name__ == "__main__":
