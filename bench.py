@@ -364,6 +364,9 @@ def parse_args(argv=None):
                          "launches overlap (two buffer sets: launch i+1's encode runs beside launch i's decode); 0: serial")
     ap.add_argument("--breakdown-steps", type=int, default=24,
                     help="--pipeline 2: launches of the pipeline-1 form run before the timed loop for the per-part times")
+    ap.add_argument("--no-plan", action="store_true",
+                    help="A/B: the encode launch writes its own code-block address stream (the offset kernel in front of "
+                         "the product on the launch stream) instead of taking the one written ahead on the side stream")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay each step as one captured HIP graph (the kernels of a step, launched together)")
     args = ap.parse_args(argv)
@@ -514,7 +517,8 @@ def run_gpu(args, dist: Dist):
             ev_start.record()
             with torch.cuda.stream(side):
                 side.wait_event(ev_start)
-                batch.encode_batch_prepare(s_, co, pieces, S["plan"], ctx_side)
+                if not args.no_plan:
+                    batch.encode_batch_prepare(s_, co, pieces, S["plan"], ctx_side)
                 ev_plan.record()
                 batch.encode_batch_headers(co, pieces, ctx_side)
                 if not args.encode_only:
@@ -522,7 +526,10 @@ def run_gpu(args, dist: Dist):
                 ev_elim.record()
             torch.cuda.current_stream().wait_event(ev_plan)
             e0.record()
-            batch.encode_batch_data_planned(s_, co, pieces, S["plan"], ctx)
+            if args.no_plan:
+                batch.encode_batch_data(s_, co, pieces, ctx)
+            else:
+                batch.encode_batch_data_planned(s_, co, pieces, S["plan"], ctx)
             if args.encode_only:
                 torch.cuda.current_stream().wait_event(ev_elim)
         else:
@@ -572,7 +579,8 @@ def run_gpu(args, dist: Dist):
                 # i-1's elimination on the side stream, long before the launch stream reaches group i's encode
                 if i >= 2:
                     side.wait_event(ev_enc[bi])
-                batch.encode_batch_prepare(s_, co, pieces, S["plan"], ctx_side)
+                if not args.no_plan:
+                    batch.encode_batch_prepare(s_, co, pieces, S["plan"], ctx_side)
                 ev_pl[bi].record()
                 if i >= 2:
                     side.wait_event(ev_done[bi])
@@ -582,7 +590,10 @@ def run_gpu(args, dist: Dist):
             if i >= 2:
                 torch.cuda.current_stream().wait_event(ev_done[bi])
             torch.cuda.current_stream().wait_event(ev_pl[bi])
-            batch.encode_batch_data_planned(s_, co, pieces, S["plan"], ctx)
+            if args.no_plan:
+                batch.encode_batch_data(s_, co, pieces, ctx)
+            else:
+                batch.encode_batch_data_planned(s_, co, pieces, S["plan"], ctx)
             ev_enc[bi].record()
             with torch.cuda.stream(s_dec):
                 s_dec.wait_event(ev_enc[bi])
@@ -762,6 +773,8 @@ def run_gpu(args, dist: Dist):
             "objects_total": int(total_objs), "objects_per_launch": C,
             "parallelism": f"objects sharded over {dist.world} rank(s), no data-path collective",
             "kernel_variant": variant,
+            "encode_address_stream": "launch stream (--no-plan)" if args.no_plan else
+                                     "written ahead on the side stream (rlnc_encode_batch_prepare)",
             "pipeline": {0: "serial", 1: "elimination on a side stream concurrent with the encode data work",
                          2: "elimination beside the encode data work, and launch group i+1's encode beside group "
                             "i's decode (two buffer sets)"}[args.pipeline],

@@ -113,7 +113,7 @@ struct CallWs {
     uint32_t epoch = 0;
     // large copy-outs to host (Decoder::get_decoded_data): a ring of pinned chunks the DMA fills while host threads
     // copy the previous chunks into the caller's buffer (engine.cpp copy_out)
-    static constexpr int kOutRing = 3;
+    static constexpr int kOutRing = 4;
     PinBuf pin_out;
     hipEvent_t out_ev[kOutRing] = {};
     CallWs() { pc_coef.flags = pc_out.flags = pc_flag.flags = hipHostMallocCoherent; }

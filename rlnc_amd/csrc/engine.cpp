@@ -1023,6 +1023,26 @@ void advise_huge(uint8_t *dst, size_t n) {
     if (on && b > a) (void)madvise(reinterpret_cast<void *>(a), b - a, MADV_HUGEPAGE);
 }
 
+// whether dst's pages are already mapped (a heap block the caller's allocator reused, zeroed on the caller's thread):
+// mincore on its first, middle and last pages -- a fresh mapping has none of them
+bool pages_resident(const uint8_t *dst, size_t n) {
+    const uintptr_t pg = 4096;
+    for (size_t off : {size_t(0), n / 2, n - 1}) {
+        unsigned char v = 0;
+        void *a = reinterpret_cast<void *>(reinterpret_cast<uintptr_t>(dst + off) & ~(pg - 1));
+        if (mincore(a, pg, &v) != 0 || !(v & 1)) return false;
+    }
+    return true;
+}
+
+bool touch_first() {
+    static const bool on = [] {
+        const char *e = getenv("RLNC_COPY_TOUCH");  // A/B knob, read once: 0 = no pre-faulting
+        return !e || atoi(e) != 0;
+    }();
+    return on;
+}
+
 int copy_out(CallWs *ws, uint8_t *dst, const uint8_t *src_dev, size_t n) {
     const int threads = copy_threads();
     if (n < kOutParallelMin || threads <= 1) {
@@ -1045,6 +1065,9 @@ int copy_out(CallWs *ws, uint8_t *dst, const uint8_t *src_dev, size_t n) {
     };
     for (size_t c = 0; c < std::min<size_t>(R, chunks); ++c)
         if (int st = issue(c)) return st;
+    // while the device runs the product and the first chunks' DMAs: fault the caller's pages in, in parallel (a fresh
+    // buffer's page faults were most of the host copies' time: profiles/r05_copyout_trace*)
+    if (touch_first() && !pages_resident(dst, n)) par_touch(dst, n, threads);
     const bool tr = g_copy_trace.on;
     const uint64_t t0 = tr ? now_ns() : 0;
     uint64_t tw = 0, tc = 0, tf = 0;

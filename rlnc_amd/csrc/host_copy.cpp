@@ -21,6 +21,7 @@ constexpr size_t kPage = 4096;
 // bandwidth-bound, two at once would not finish sooner).
 class Pool {
    public:
+    // src == nullptr: touch instead of copy (one zero byte per 4 KiB page of each slice)
     void run(uint8_t *dst, const uint8_t *src, size_t n, int threads) {
         std::lock_guard<std::mutex> call(call_mu_);
         ensure(threads - 1);
@@ -37,7 +38,7 @@ class Pool {
             pending_ = slices_ - 1;
         }
         cv_.notify_all();
-        std::memcpy(dst, src, std::min(per, n));
+        copy_slice(0);
         std::unique_lock<std::mutex> lock(mu_);
         // the caller takes slices too until none is left unclaimed, then waits for the workers' last ones
         while (next_ < slices_) {
@@ -53,7 +54,11 @@ class Pool {
    private:
     void copy_slice(size_t s) {
         const size_t a = s * per_, b = std::min(n_, a + per_);
-        std::memcpy(dst_ + a, src_ + a, b - a);
+        if (src_ != nullptr) {
+            std::memcpy(dst_ + a, src_ + a, b - a);
+        } else {
+            for (size_t i = a; i < b; i += kPage) reinterpret_cast<volatile uint8_t *>(dst_)[i] = 0;
+        }
     }
     void ensure(int workers) {
         while (int(workers_) < workers) {
@@ -86,6 +91,15 @@ Pool &pool() {
 }
 
 }  // namespace
+
+void par_touch(void *dst, size_t n, int threads) {
+    threads = int(std::min<size_t>(size_t(std::max(1, threads)), n / kMinSlice));
+    if (threads <= 1) {
+        for (size_t i = 0; i < n; i += kPage) static_cast<volatile uint8_t *>(dst)[i] = 0;
+        return;
+    }
+    pool().run(static_cast<uint8_t *>(dst), nullptr, n, threads);
+}
 
 int copy_threads() {
     static const int t = [] {

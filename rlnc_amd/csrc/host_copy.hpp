@@ -13,6 +13,9 @@ namespace rlnc::eng {
 // dst[0, n) = src[0, n) with up to `threads` threads (the caller's included); returns when done.  Small copies stay on
 // the calling thread.
 void par_copy(void *dst, const void *src, size_t n, int threads);
+// the pages of dst[0, n) faulted in (one zero byte written per 4 KiB) by up to `threads` threads: a caller buffer
+// fresh from calloc is then warm when the device's bytes arrive (call it while the device works)
+void par_touch(void *dst, size_t n, int threads);
 // the thread count par_copy callers use: RLNC_COPY_THREADS (A/B knob, read once), else min(8, hardware threads)
 int copy_threads();
 
