@@ -1,0 +1,22 @@
+# round-5 closing measurements: both GPU suites, smoke, the default bench line, a rocprofv3 kernel trace of the same
+# command with the breakdown launches selected, every config, an object-API grid run
+set -o pipefail
+O=gpurun_out/r05_final
+mkdir -p $O
+R=$PWD
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+RLNC_LIB_PATH=$R/rlnc_amd/librlnc_hip_ab.so timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_fullrange.py tests/test_gpu_graph.py > $O/ab_tests.log 2>&1 || { tail -40 $O/ab_tests.log; exit 1; }
+tail -1 $O/ab_tests.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+grep '^{' $O/bench.json | cut -c1-300
+( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof_bench -o run -- python $R/bench.py --no-cpu-baseline > $R/$O/prof_bench.json 2> $R/$O/prof_bench.log ) || { tail $O/prof_bench.log; exit 1; }
+python3 scripts/rocpd_stats.py $O/prof_bench/run_results.db > $O/bench_kernel_stats.csv
+python3 scripts/breakdown_launches.py $O/prof_bench/run_results.db $O/prof_bench.json > $O/breakdown_launches.json
+cat $O/breakdown_launches.json
+timeout -k 10 400 python scripts/bench_configs.py > $O/configs.jsonl 2> $O/configs.err || { tail $O/configs.err; exit 1; }
+cat $O/configs.jsonl | cut -c1-200
+timeout -k 10 600 build/object_api_bench > $O/object_api_grid.jsonl 2> $O/object_api_grid.err || { tail $O/object_api_grid.err; exit 1; }
+echo "all done"
