@@ -925,3 +925,63 @@ def test_encode_plan_written_ahead(orc, variant, k, L, n):
     c1.close()
     c2.close()
 
+
+
+@pytest.mark.parametrize("k", [16, 8, 5])
+def test_decode_small_objects_marker_outcomes(ctx, k):
+    """Objects of k <= 16 pieces x one 4 KiB column block (the small-object elimination + 1- / 2-wave product, then
+    the marker scan of decoder.rs:162-177, 16 lanes an object).  Payload tails chosen to hit every outcome: the marker as the very last byte, early in row 0, alone at the start of the last row, at index 0 only
+    (invalid), an all-zero payload (invalid), a last nonzero byte other than 0x81 (invalid), and rank-deficient
+    objects (NotAllPiecesReceivedYet, length 0)."""
+    import torch
+
+    from rlnc_amd import batch
+
+    nobj, L = 2056, 4096
+    rng = np.random.default_rng(77 + k)
+    src = rng.integers(0, 256, (nobj, k * L), dtype=np.uint8)
+    want_len = np.zeros(nobj, np.int64)
+    for o in range(nobj):
+        c = o % 6
+        if c == 0:
+            src[o, -1] = 0x81
+            want_len[o] = k * L - 1
+        elif c == 1:
+            src[o, 101:] = 0
+            src[o, 100] = 0x81
+            want_len[o] = 100
+        elif c == 2:
+            src[o] = 0
+        elif c == 3:
+            src[o] = 0
+            src[o, 0] = 0x81
+        elif c == 4:
+            src[o, -1] = 0x7E
+        else:
+            src[o, (k - 1) * L:] = 0
+            src[o, (k - 1) * L] = 0x81
+            want_len[o] = (k - 1) * L
+    co = rng.integers(0, 256, (nobj, k, k), dtype=np.uint8)
+    deficient = np.arange(nobj) % 11 == 7
+    co[deficient, 1] = co[deficient, 0]  # a repeated coding vector: rank k - 1 at most
+    src_d = dev(src.reshape(nobj, k, L))
+    pieces = torch.empty((nobj, k, k + L), dtype=torch.uint8, device=src_d.device)
+    batch.encode_batch(src_d, dev(co), pieces, ctx)
+    decoded = dev(np.zeros((nobj, k, L), np.uint8))
+    pst, ost, dl = batch.decode_batch(pieces, k, decoded, ctx)
+    got = host(decoded).reshape(nobj, k * L)
+    for o in range(nobj):
+        od = OracleDecoder(L, k)
+        for p in host(pieces[o]):
+            od.decode(p)
+        st, data = od.get_decoded_data()
+        assert S[ost[o]] == S[st], o
+        assert int(dl[o]) == (len(data) if S[st] == "Ok" else 0), o
+        if deficient[o] or S[st] == "NotAllPiecesReceivedYet":  # (a random 16 x 16 matrix is singular at ~1/256)
+            assert S[ost[o]] == "NotAllPiecesReceivedYet", o
+            continue
+        assert np.array_equal(got[o], src[o]), o
+        if o % 6 in (0, 1, 5):
+            assert S[ost[o]] == "Ok" and int(dl[o]) == want_len[o], o
+        else:
+            assert S[ost[o]] == "InvalidDecodedDataFormat", o

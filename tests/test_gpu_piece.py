@@ -164,3 +164,47 @@ def test_get_decoded_data_recovers_source(ctx, size, k):
             pass
     got = dec.get_decoded_data()
     assert np.array_equal(got, data)
+
+
+def test_get_decoded_data_large_objects_from_threads(ctx):
+    """Large decodes' copy-out (pinned ring + the host copy pool, pre-faulting fresh caller buffers) from four threads
+    at once, each on its own decoder of a 9-33 MiB object (fresh numpy buffers above glibc's mmap threshold and heap
+    reuse below it): every result equals its source.  The pool serialises concurrent copies; each call's ring and
+    events are its own workspace's."""
+    import threading
+
+    from rlnc_amd.full import Decoder, Encoder
+
+    sizes = [(33 << 20) + 5, (9 << 20) + 77, (16 << 20) - 3, (24 << 20) + 1]
+    decs, datas = [], []
+    for i, size in enumerate(sizes):
+        rng = np.random.default_rng(500 + i)
+        data = rng.integers(0, 256, size, dtype=np.uint8)
+        k = 16 if i % 2 else 32
+        enc = Encoder.new(data, k, ctx)
+        dec = Decoder.new(enc.get_piece_byte_len(), k, ctx)
+        while not dec.is_already_decoded():
+            try:
+                dec.decode(enc.code(rng))
+            except Exception:
+                pass
+        decs.append(dec)
+        datas.append(data)
+    results = [None] * len(decs)
+    errors = []
+
+    def work(i):
+        try:
+            for _ in range(2):  # the second call reuses the same workspace pool and pinned ring
+                results[i] = decs[i].get_decoded_data()
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(len(decs))]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errors, errors
+    for got, data in zip(results, datas):
+        assert np.array_equal(got, data)
