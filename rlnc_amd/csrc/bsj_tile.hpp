@@ -49,13 +49,22 @@ __device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stre
     }
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    const int rows_w = __builtin_amdgcn_readfirstlane(max(0, min(kBsjWaveRows, rows - kBsjWaveRows * w)));
+    // the split 2-wave program (gen_bsjump.py --w2split): wave w owns the 2 KiB half w of the column block in all
+    // the tile's rows, instead of rows [8 w, 8 w + 8) in the whole block
+#ifdef RLNC_BSJ_W2SPLIT
+    constexpr bool kSplit = W == 2;
+#else
+    constexpr bool kSplit = false;
+#endif
+    const int wr = kSplit ? 0 : w;  // the wave's first row in the tile (in wave rows)
+    const int rows_w =
+        __builtin_amdgcn_readfirstlane(kSplit ? rows : max(0, min(kBsjWaveRows, rows - kBsjWaveRows * w)));
     const uint8_t *src = p.in + int64_t(obj) * p.in_obj + int64_t(cb) * kBsjColBlock;
-    uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0 + kBsjWaveRows * w) * p.out_row +
-                   int64_t(cb) * kBsjColBlock;
+    uint8_t *dst = p.out + int64_t(obj) * p.out_obj + int64_t(row0 + kBsjWaveRows * wr) * p.out_row +
+                   int64_t(cb) * kBsjColBlock + (kSplit ? 2048 * w : 0);
     constexpr int kEntry = SHARE ? 8 : 4;  // bytes per stream entry: absolute address / block offset
     const uint8_t *idx = static_cast<const uint8_t *>(stream) +
-                         ((int64_t(obj) * row_tiles + rt) * p.n_in * kTileRows + kBsjWaveRows * w) * kEntry;
+                         ((int64_t(obj) * row_tiles + rt) * p.n_in * kTileRows + kBsjWaveRows * wr) * kEntry;
     typedef __attribute__((address_space(3))) uint8_t lds_u8;
     const uint32_t ring_lds = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)ring));  // addrspacecast
     // W = 8 (shared): waves 0-3 stage the ring and build the sets exactly as in the 4-wave program, waves 4-7
@@ -69,7 +78,7 @@ __device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stre
     const uint32_t off = 16u * lane;
     const uint32_t ldsc = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)cset)) + 16u * lane;
     const uint32_t ldscw = ldsc + 4096u * uint32_t(ws);      // this wave's set (group ws >> 1, half ws & 1)
-    const uint32_t ldsrg = ldsr + 2048u * uint32_t(ws >> 1);  // this wave's group of the ring chunk
+    const uint32_t ldsrg = ldsr + 2048u * uint32_t(kSplit ? ws : ws >> 1);  // this wave's group of the ring chunk
     const uint32_t half = uint32_t(ws & 1);
     const uint32_t cons = uint32_t(w / kStageWaves);
 #pragma clang diagnostic push

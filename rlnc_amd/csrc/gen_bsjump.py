@@ -871,6 +871,139 @@ def program(slots=SLOTS):
     return L
 
 
+# ---- split 2-wave program (--w2split) ----------------------------------------------------------------------
+# Tiles of <= 16 rows (many small objects: configs[0]'s 16 x 4 KiB): wave w owns byte group w of every lane (the 2 KiB
+# half [2048 w, 2048 w + 2 KiB) of the column block) for ALL 16 rows, instead of both groups of 8 rows.  A wave then
+# transposes and combines one group per source row instead of two (half the set building, which is ~20 % of the
+# 2-wave program on configs[0]: profiles/r05_sets_ab.jsonl), and it reads only the half of the ring chunk it moved in by
+# DMA itself, so the two waves never wait for each other (no barrier).  The price: 16 calls of 8 XOR3s per source row
+# instead of 8 calls of 16.  Same block-offset stream as the 2-wave program (16 entries per source row, both waves read
+# all 16), same 136-byte block stride (blocks half used).
+SPLIT_NT = 16
+
+
+def ACCS(i, p):  # row i (0..15), plane p of the wave's group
+    return 8 * i + p
+
+
+def GS(h, v):  # combination v of half h of the wave's group
+    return 128 + 16 * h + v
+
+
+def RAWS(d):
+    return 160 + d
+
+
+SPLIT_MAP = dict(TMP0=168, V_X=176, V_MASK=(184, 185, 186))
+SPLIT_SGPRS = dict(S_OFF=(36, 52), S_SRC=68, S_IDX=70, S_DST=72, S_BASE=74, S_TGT=76, S_RET=78, S_INROW=80,
+                   S_OUTROW=81, S_CNT=82, S_ROWS=83, S_T0=84, S_LDSW=85)
+
+
+def call_split(L, cur, i):
+    L += [f"s_mov_b32 m0, {hex(0xC000 | (8 * i))}", f"s_add_u32 s{S_TGT}, s{S_BASE}, s{cur + i}"]
+    if not FAST:
+        L.append(f"s_addc_u32 s{S_TGT + 1}, s{S_BASE + 1}, 0")
+    L.append(f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{S_TGT}:{S_TGT + 1}]")
+
+
+def body_split(L, j):
+    """Source row j (ring slot j % 3, offset buffer j % 2): this wave's own DMA of it done, then its group's set."""
+    slot = j % SLOTS
+    L += [f"s_waitcnt vmcnt({4 // WAVES})",  # this wave's DMAs of row j done (row j + 1's may fly)
+          f"s_sub_u32 s{S_CNT}, s{S_CNT}, 1"]
+    advance(L)
+    dma(L, (slot + 2) % SLOTS)  # row j + 2 into the slot row j - 1 used (read and waited for in row j - 1)
+    for h in range(2):
+        L.append(f"ds_read_b128 v[{RAWS(4 * h)}:{RAWS(4 * h) + 3}], %[ldsrg] offset:{slot * 4096 + h * 1024}")
+    L.append("s_waitcnt lgkmcnt(0)")  # the chunk, and row j's block offsets (SMEM, issued a row earlier)
+    transpose({d: RAWS(d) for d in range(8)}, {b: GS(b // 4, 1 << (b % 4)) for b in range(8)}, L)
+    for h in range(2):
+        b = lambda x: v(GS(h, x))
+        L += [f"v_xor_b32 {b(x)}, {b(y)}, {b(z)}" for x, y, z in
+              [(3, 1, 2), (5, 1, 4), (6, 2, 4), (7, 3, 4), (9, 1, 8), (10, 2, 8), (11, 3, 8), (12, 4, 8), (13, 5, 8),
+               (14, 6, 8), (15, 7, 8)]]
+    cur, nxt = S_OFF[j % 2], S_OFF[(j + 1) % 2]
+    L += [f"s_load_dwordx16 s[{nxt}:{nxt + 15}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
+          f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
+          f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
+          "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)"]
+    for i in range(SPLIT_NT):
+        call_split(L, cur, i)
+    L.append("s_set_gpr_idx_off")
+
+
+def blocks_split(L):
+    for c in range(256):
+        lo, hi = block_indices(c)
+        if c == 0:
+            L.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+            L += ["s_nop 0"] * ((BLOCK_BYTES - 4) // 4)
+            continue
+        for o in range(8):
+            a = ACCS(0, o)
+            if lo[o] == 0 and hi[o] == 0:
+                L += ["s_nop 0", "s_nop 0"]
+                continue
+            x = f"v{GS(0, lo[o])}" if lo[o] else "0"
+            y = f"v{GS(1, hi[o])}" if hi[o] else "0"
+            L.append(f"v_bitop3_b32 v{a}, {x}, {y}, v{a} bitop3:0x96")
+        L.append(f"s_setpc_b64 s[{S_RET}:{S_RET + 1}]")
+        L += ["s_nop 0"] * ((BLOCK_BYTES - (8 * 8 + 4)) // 4)
+
+
+def epilogue_split(L):
+    for i in range(SPLIT_NT):
+        L += [f"s_cmp_gt_u32 s{S_ROWS}, {i}", "s_cbranch_scc0 2f"]
+        transpose({p: ACCS(i, p) for p in range(8)}, {d: V_X + d for d in range(8)}, L)
+        for half in range(2):
+            off = f" offset:{half * 1024}" if half else ""
+            L.append(f"global_store_dwordx4 %[off], v[{V_X + 4 * half}:{V_X + 4 * half + 3}], s[{S_DST}:{S_DST + 1}]{off}")
+        L += [f"s_add_u32 s{S_DST}, s{S_DST}, s{S_OUTROW}", f"s_addc_u32 s{S_DST + 1}, s{S_DST + 1}, 0"]
+    L.append("2:")
+
+
+def program_split():
+    assert WAVES == 2 and STREAM_J_BYTES == 4 * SPLIT_NT
+    saved = {n: globals()[n] for n in list(SPLIT_MAP) + list(SPLIT_SGPRS)}
+    globals().update(SPLIT_MAP)
+    globals().update(SPLIT_SGPRS)
+    try:
+        L = [
+            f"s_mov_b64 s[{S_SRC}:{S_SRC + 1}], %[src]",
+            f"s_mov_b64 s[{S_IDX}:{S_IDX + 1}], %[idx]",
+            f"s_mov_b64 s[{S_DST}:{S_DST + 1}], %[dst]",
+            f"s_mov_b32 s{S_INROW}, %[in_row]",
+            f"s_mov_b32 s{S_OUTROW}, %[out_row]",
+            f"s_mov_b32 s{S_CNT}, %[n_in]",
+            f"s_mov_b32 s{S_ROWS}, %[rows]",
+            f"v_mov_b32 v{V_MASK[0]}, 0xaaaaaaaa",
+            f"v_mov_b32 v{V_MASK[1]}, 0xcccccccc",
+            f"v_mov_b32 v{V_MASK[2]}, 0xf0f0f0f0",
+            f"s_getpc_b64 s[{S_BASE}:{S_BASE + 1}]",
+            "5:",
+            f"s_add_u32 s{S_BASE}, s{S_BASE}, (9f - 5b)",
+            f"s_addc_u32 s{S_BASE + 1}, s{S_BASE + 1}, 0",
+            f"s_mov_b32 s{S_LDSW}, %[ldsw]",
+        ]
+        dma(L, 0)
+        advance(L)
+        dma(L, 1)
+        L.append(f"s_load_dwordx16 s[{S_OFF[0]}:{S_OFF[0] + 15}], s[{S_IDX}:{S_IDX + 1}], 0")
+        L += [f"v_mov_b32 v{r}, 0" for r in range(8 * SPLIT_NT)]
+        L += [f"v_mov_b32 v{GS(h, 0)}, 0" for h in range(2)]
+        loops(L, body_split, 6)  # lcm of the 3 ring slots and the 2 offset buffers
+        epilogue_split(L)
+        L.append("s_branch 8f")
+        if ALIGN:
+            L.append(f".p2align {ALIGN}")
+        L.append("9:")
+        blocks_split(L)
+        L.append("8:")
+        return L
+    finally:
+        globals().update(saved)
+
+
 # cache-policy modifiers of the source DMA loads and the tile stores (--load-hint / --store-hint, A/B only; the
 # default program carries none)
 HINTS = {"load": "", "store": ""}
@@ -911,6 +1044,7 @@ def main():
     # 4,096 x 16 x 4 KiB encode 0.149 -> 0.142 ms, decode 0.179 -> 0.169 (profiles/r04_hint_cfg0_ab.txt); the 4- and
     # 8-wave programs keep plain stores (no gain on the VALU-bound bench, profiles/r02_cache_hint_ab.txt)
     ap.add_argument("--store-hint-small", default="nt", help="tile-store modifiers of the 1- and 2-wave programs")
+    ap.add_argument("--w2split", action="store_true", help="2-wave program: waves split the byte groups, not the rows")
     args = ap.parse_args()
     HINTS["load"], HINTS["store"] = args.load_hint, args.store_hint
     global PRIO_AT
@@ -936,13 +1070,18 @@ def main():
         f.write(f"#define RLNC_BSJ_BLOCK_BYTES {BLOCK_BYTES}\n")
         f.write(f"#define RLNC_BSJ_SLOTS1 {args.slots1}\n")
         f.write(f"#define RLNC_BSJ_SLOTS2 {args.slots2}\n")
+        if args.w2split:
+            f.write("#define RLNC_BSJ_W2SPLIT 1\n")
         for w in (1, 2, 4):
             WAVES, WG_ROWS = w, NT * w
             STREAM_J_BYTES = WG_ROWS * 4
             saved = HINTS["store"]
             if w <= 2 and not HINTS["store"]:
                 HINTS["store"] = args.store_hint_small
-            body_txt = "\\n\\t".join(hinted(program({1: args.slots1, 2: args.slots2}.get(w, SLOTS))))
+            if w == 2 and args.w2split:
+                body_txt = "\\n\\t".join(hinted(program_split()))
+            else:
+                body_txt = "\\n\\t".join(hinted(program({1: args.slots1, 2: args.slots2}.get(w, SLOTS))))
             HINTS["store"] = saved
             f.write(f'#define RLNC_BSJ_ASM_W{w} "{body_txt}"\n')
         WAVES, WG_ROWS = 4, NT * 4
