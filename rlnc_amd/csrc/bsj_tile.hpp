@@ -6,7 +6,9 @@
 
 #include <cstdint>
 
+#include "../../include/rlnc_hip.h"
 #include "bitslice_jump.inc"
+#include "gf256.hpp"
 #include "kernels.hpp"
 
 #ifndef RLNC_BSJ_SOFFSETS
@@ -27,6 +29,58 @@ constexpr int kBsjColBlock = 4096;          // 64 lanes × 64 B, shared by the W
 // first tile pays the prologue (first DMAs, first sets); the grid is objects x row tiles x runs
 // The tile of one workgroup: output rows [rt * 8W, +8W) x column block cb of object obj (the uniform batch
 // kernel below and the ragged kernel both end here).
+// The marker scan of an object whose tile this workgroup holds whole (MatmulParams::scan_need; decoder.rs:162-177: the
+// last nonzero byte of the padded payload must be the 0x81 marker, not at index 0), for objects whose payload tail the
+// elimination found all zero: every wave's tile stores done and visible to the workgroup, then wave 0 walks the rows
+// from the last one, 64 B a lane, the last nonzero byte found by a wave max (DPP row rotations + permlane swaps) of
+// (offset + 1) << 8 | byte.  (rank < k never gets here: the elimination answered NotAllPiecesReceivedYet.)
+__device__ __forceinline__ uint32_t tile_wave_max(uint32_t a) {
+    a = max(a, uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x121, 0xf, 0xf, false)));  // row_ror:1
+    a = max(a, uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x122, 0xf, 0xf, false)));  // row_ror:2
+    a = max(a, uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x124, 0xf, 0xf, false)));  // row_ror:4
+    a = max(a, uint32_t(__builtin_amdgcn_update_dpp(0, int(a), 0x128, 0xf, 0xf, false)));  // row_ror:8
+    const auto s16 = __builtin_amdgcn_permlane16_swap(a, a, false, false);
+    a = max(s16[0], s16[1]);
+    const auto s32 = __builtin_amdgcn_permlane32_swap(a, a, false, false);
+    return max(s32[0], s32[1]);
+}
+
+__device__ __forceinline__ void bsj_tile_scan(const MatmulParams &p, int obj) {
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's tile stores (issued inside the program)
+    __syncthreads();                                       // ... and every other wave's
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    const uint8_t *base = p.out + int64_t(obj) * p.out_obj;
+    int64_t hit = -1;
+    uint32_t byte = 0;
+    for (int r = p.scan_k - 1; r >= 0; --r) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(base + int64_t(r) * p.out_row + 64 * lane);
+        uint32_t mine = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint4 x = q[u];
+            const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (w[t]) {
+                    const int b = (31 - __builtin_clz(w[t])) / 8;
+                    mine = (uint32_t(64 * lane + 16 * u + 4 * t + b + 1) << 8) | ((w[t] >> (8 * b)) & 0xFFu);
+                }
+        }
+        const uint32_t best = __builtin_amdgcn_readfirstlane(tile_wave_max(mine));
+        if (best) {
+            hit = int64_t(r) * p.width + int64_t(best >> 8) - 1;
+            byte = best & 0xFFu;
+            break;
+        }
+    }
+    if (lane == 0) {
+        const bool ok = hit > 0 && byte == kBoundaryMarker;
+        p.scan_status[obj] = ok ? RLNC_OK : RLNC_ERR_INVALID_DECODED_DATA_FORMAT;
+        p.scan_len[obj] = ok ? hit : 0;
+    }
+}
+
 template <int W, bool SHARE, bool RUN>
 __device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stream, int row_tiles, int rt, int cb,
                                          int obj, uint32_t tiles, uint64_t *probe) {
@@ -98,6 +152,8 @@ __device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stre
     if constexpr (W == 8 && RUN) asm volatile(RLNC_BSJ_ASM_W8R : RLNC_BSJ_OPERANDS);
 #undef RLNC_BSJ_OPERANDS
 #pragma clang diagnostic pop
+    if constexpr (W <= 2 && !SHARE && !RUN)
+        if (p.scan_status != nullptr && p.scan_need[obj] != 0) bsj_tile_scan(p, obj);
 }
 
 }  // namespace

@@ -204,7 +204,8 @@ struct rlnc_context {
                           // 3 device elimination with the clean state on LDS, 4 ... on one wave's
                           // registers, 5 blocked clean run, 6 round-1 multi-wave registers (A/B)
     // workspaces of the stream-ordered batch / _device API (one caller thread per context at a time)
-    DevBuf ws_bsj;  // the small-object decode's block-offset stream, written by its elimination
+    DevBuf ws_bsj;   // the small-object decode's block-offset stream, written by its elimination
+    DevBuf ws_need;  // ... and its per-object "payload tail all zero" flags (RrefParams::tail_need)
     DevBuf ws_coef, ws_out, ws_status, ws_len, ws_pstat, ws_rank, ws_idx;
     PinBuf pin_a, pin_b, pin_c;
     // set once a batch call ran inside a HIP stream capture: the graph holds the workspace addresses, so
@@ -457,7 +458,8 @@ struct rlnc_context {
             const int total = p.n_out;
             for (int r0 = 0; r0 < total; r0 += max_tile_rows) {
                 rlnc::MatmulParams q = p;
-                q.bsj_stream = nullptr;  // laid out for all the rows
+                q.bsj_stream = nullptr;   // laid out for all the rows
+                q.scan_status = nullptr;  // rows split over launches: no workgroup holds a whole object
                 q.n_out = std::min(max_tile_rows, total - r0);
                 q.coef = p.coef + int64_t(r0) * p.coef_row;
                 q.out = p.out + int64_t(r0) * p.out_row;

@@ -1320,9 +1320,18 @@ int rlnc_recode_batch(rlnc_context *ctx, const uint8_t *pieces, size_t k, size_t
 // Everything is enqueued on the context stream; outputs stay on the device.
 // The elimination alone: reads only the k coefficient bytes of each piece; writes T [obj][k][m], the per-piece
 // statuses and the ranks.
+// tail (optional, with bsj): the small-object elimination also answers get_final_data_len from the payload tail
+// (RrefParams::tail_status): {status, length, need-scan flags} device arrays
+struct TailOut {
+    int32_t *status = nullptr;
+    int64_t *len = nullptr;
+    int32_t *need = nullptr;
+};
+
 static int decode_eliminate_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
                                  size_t m, size_t nobj, uint8_t *T, int32_t *pstat_dev, int32_t *rank_dev,
-                                 uint32_t *bsj = nullptr, int bsj_rows = 0, bool *bsj_written = nullptr) {
+                                 uint32_t *bsj = nullptr, int bsj_rows = 0, bool *bsj_written = nullptr,
+                                 const TailOut *tail = nullptr) {
     const size_t full = k + L;
     rlnc::RrefParams rp{};
     rp.pieces = pieces;
@@ -1341,14 +1350,30 @@ static int decode_eliminate_impl(rlnc_context *ctx, const uint8_t *pieces, size_
     rp.bsj_stream = bsj;
     rp.bsj_block_bytes = rlnc::bsj_block_bytes_public();
     rp.bsj_tile_rows = bsj_rows;
+    if (tail != nullptr) {
+        rp.tail_status = tail->status;
+        rp.tail_len = tail->len;
+        rp.tail_need = tail->need;
+        rp.tail_L = int64_t(L);
+    }
     HIP_TRY(rlnc::launch_rref_batch(rp, ctx->stream, bsj_written));
     return RLNC_OK;
+}
+
+// RLNC_FUSED_SCAN=0 (A/B knob, read once): the separate marker-scan launch for every decode
+static bool fused_scan_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("RLNC_FUSED_SCAN");
+        return !e || atoi(e) != 0;
+    }();
+    return on;
 }
 
 // The data side: decoded = T × received data (one matmul), then the marker scan (decoder.rs:136-177).
 static int decode_apply_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
                              size_t m, size_t nobj, const uint8_t *T, const int32_t *rank_dev, uint8_t *decoded,
-                             int32_t *ostat_dev, int64_t *len_dev, const void *bsj = nullptr, int bsj_rows = 0) {
+                             int32_t *ostat_dev, int64_t *len_dev, const void *bsj = nullptr, int bsj_rows = 0,
+                             const int32_t *need_dev = nullptr) {
     const size_t full = k + L;
     int st;
     rlnc::MatmulParams p{};
@@ -1367,9 +1392,21 @@ static int decode_apply_impl(rlnc_context *ctx, const uint8_t *pieces, size_t ob
     p.n_obj = int(nobj);
     p.bsj_stream = bsj;
     p.bsj_stream_rows = bsj_rows;
+    // need_dev: the elimination already wrote every object's status and length from its payload tail; the objects
+    // whose tail was all zero are scanned by their product workgroup when each object is one tile (configs[0]'s shape),
+    // else the scan kernel runs over all of them
+    bool scanned = false;
+    if (need_dev != nullptr) {
+        p.scan_status = ostat_dev;
+        p.scan_need = need_dev;
+        p.scan_len = len_dev;
+        p.scan_k = int(k);
+        p.scan_done = &scanned;
+    }
     if ((st = ctx->matmul(p))) return st;
-    HIP_TRY(rlnc::launch_final_data_len_ranked(decoded, int64_t(k * L), int64_t(k * L), int(nobj), int(k), rank_dev,
-                                               ostat_dev, len_dev, ctx->stream));
+    if (!scanned)
+        HIP_TRY(rlnc::launch_final_data_len_ranked(decoded, int64_t(k * L), int64_t(k * L), int(nobj), int(k), rank_dev,
+                                                   ostat_dev, len_dev, ctx->stream));
     return RLNC_OK;
 }
 
@@ -1390,12 +1427,23 @@ static int decode_batch_device_impl(rlnc_context *ctx, const uint8_t *pieces, si
         if ((st = ctx->grow(ctx->ws_bsj, nobj * m * size_t(bsj_rows) * 4 + 512))) return st;
         bsj = ctx->ws_bsj.as<uint32_t>();
     }
+    // one-tile objects (k <= 16 x one 4 KiB column block): the elimination answers the marker scan from the payload
+    // tail and the product's workgroups scan the rare all-zero tails (no scan launch: configs[0] shape)
+    TailOut tail;
+    const bool want_tail = bsj != nullptr && L == 4096 && k % 4 == 0 && obj_stride % 4 == 0 &&
+                           reinterpret_cast<uintptr_t>(pieces) % 4 == 0 && fused_scan_enabled();
+    if (want_tail) {
+        if ((st = ctx->grow(ctx->ws_need, nobj * 4))) return st;
+        tail.status = ostat_dev;
+        tail.len = len_dev;
+        tail.need = ctx->ws_need.as<int32_t>();
+    }
     bool written = false;
     if ((st = decode_eliminate_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, pstat_dev, rank_dev, bsj, bsj_rows,
-                                    &written)))
+                                    &written, want_tail ? &tail : nullptr)))
         return st;
     return decode_apply_impl(ctx, pieces, obj_stride, k, L, m, nobj, T, rank_dev, decoded, ostat_dev, len_dev,
-                             written ? bsj : nullptr, written ? bsj_rows : 0);
+                             written ? bsj : nullptr, written ? bsj_rows : 0, written && want_tail ? tail.need : nullptr);
 }
 
 // Host path (matrices too large for LDS): exact elimination on host threads (elimination.hpp).

@@ -679,6 +679,12 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
     if (e != hipSuccess) return e;
     MatmulParams q = p;
     q.width = b.full;
+    // the marker scan of undecided objects in the tiles (MatmulParams::scan_need) when each object is one workgroup's
+    // whole tile (the 1- and 2-wave programs are never the shared ones, whatever b.share says)
+    const bool scan = p.scan_status != nullptr && p.scan_need != nullptr && b.waves <= 2 && b.row_tiles == 1 &&
+                      b.col_blocks == 1 && b.full == p.width && p.width == kBsjColBlock && p.n_out == p.scan_k &&
+                      p.out_row == p.width && p.out_obj == int64_t(p.scan_k) * p.width;
+    if (!scan) q.scan_status = nullptr;
     const dim3 grid(unsigned(b.total));
     if (b.waves == 1)
         hipLaunchKernelGGL(gf_matmul_bsj_kernel<1>, grid, dim3(64), 0, s, q, b.stream, b.row_tiles, b.col_blocks,
@@ -695,7 +701,9 @@ hipError_t launch_bsj(const MatmulParams &p, hipStream_t s, void *scratch, size_
     else
         hipLaunchKernelGGL(gf_matmul_bsj_kernel<4>, grid, dim3(256), 0, s, q, b.stream, b.row_tiles, b.col_blocks,
                            nullptr);
-    return hipGetLastError();
+    const hipError_t e2 = hipGetLastError();
+    if (e2 == hipSuccess && scan && p.scan_done != nullptr) *p.scan_done = true;
+    return e2;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1371,7 +1379,11 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
     if (p.n_out <= 0 || p.width <= 0 || p.n_obj <= 0) return hipSuccess;
     const bool aligned = matmul_aligned(p);
     if (p.n_in <= 0) return hipErrorInvalidValue;
-    if (!shipped_variant(v)) return launch_matmul_ab(p, s, v, scratch, scratch_bytes);
+    if (!shipped_variant(v)) {  // the A/B variants never take the in-tile marker scan
+        MatmulParams q = p;
+        q.scan_status = nullptr;
+        return launch_matmul_ab(q, s, v, scratch, scratch_bytes);
+    }
     RealignPlan r;
     if (realign_plan(p, v, r)) {  // misaligned rows: realign copies around the aligned product
         if (scratch == nullptr || scratch_bytes < r.prod_bytes + r.in_bytes + r.out_bytes) return hipErrorInvalidValue;
@@ -1382,7 +1394,8 @@ hipError_t launch_matmul(const MatmulParams &p, hipStream_t s, MatmulVariant v, 
             for (int64_t c0 = 0; c0 < p.width; c0 += r.cw) {
                 const int64_t w = std::min(r.cw, p.width - c0);
                 MatmulParams q = p;
-                q.bsj_stream = nullptr;  // laid out for the whole batch
+                q.bsj_stream = nullptr;   // laid out for the whole batch
+                q.scan_status = nullptr;  // chunks of columns: no workgroup holds a whole object
                 q.n_obj = c;
                 q.width = w;
                 q.in = p.in + int64_t(o0) * p.in_obj + c0;

@@ -35,6 +35,16 @@ struct MatmulParams {
     // 1: bsj_stream holds the shared programs' 8-byte absolute block addresses instead (launch_bsj_stream, written
     // ahead on another stream: the encode's block-address stream off the launch stream's critical path)
     int bsj_stream_abs = 0;
+    // optional (the small-object decode, RrefParams::tail_need): objects that are ONE workgroup's tile of the 1- / 2-wave
+    // bit-sliced program (n_out = scan_k <= 16 rows, width = out_row = one 4 KiB column block) and whose final length
+    // the elimination could not decide from the payload tail (scan_need[obj] != 0) are scanned by that workgroup once
+    // its stores are done (decoder.rs:162-177) -- the marker scan without a launch of its own; launch_matmul sets
+    // *scan_done (a host flag) when it took this form, else the caller runs the scan kernel
+    int32_t *scan_status = nullptr;
+    const int32_t *scan_need = nullptr;
+    int64_t *scan_len = nullptr;
+    int scan_k = 0;
+    bool *scan_done = nullptr;
 };
 
 enum class MatmulVariant : int {
@@ -171,6 +181,15 @@ struct RrefParams {
     uint32_t *bsj_stream = nullptr;
     uint32_t bsj_block_bytes = 0;
     int bsj_tile_rows = 0;
+    // optional, with bsj_stream (same kernel): get_final_data_len (decoder.rs:162-177) decided from the last 256
+    // payload bytes -- decoded row k - 1's last 256 bytes computed from T and the pieces' tails (tail_L = L, a multiple
+    // of 4, >= 256; k a multiple of 4): tail_status / tail_len the object's status and final length when its last
+    // nonzero byte lies there (or rank < k), else tail_need[o] = 1 (the product's workgroup scans the whole payload,
+    // MatmulParams::scan_need)
+    int32_t *tail_status = nullptr;
+    int64_t *tail_len = nullptr;
+    int32_t *tail_need = nullptr;
+    int64_t tail_L = 0;
     // diagnostic build only (rref_ab.hip, RLNC_SMALL_PROF): per-wave phase timestamps of the small-object kernel
     uint64_t *prof = nullptr;
 };

@@ -95,11 +95,13 @@ hipError_t launch_rref_batch(const RrefParams &p, hipStream_t s, bool *bsj_writt
         a.m = 256 - p.k;
         a.m_stride = p.m;
         a.bsj_stream = nullptr;
+        a.tail_status = nullptr;
         hipError_t e = launch_rref_one(a, s, nullptr);
         if (e != hipSuccess) return e;
         RrefParams b = p;
         b.skip_full = 1;
         b.bsj_stream = nullptr;
+        b.tail_status = nullptr;
         return launch_rref_one(b, s, nullptr);
     }
     return launch_rref_one(p, s, bsj_written);

@@ -1149,6 +1149,46 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 
         for (int s = lane / tr; s < m; s += step)
             st[s * tr + r] = (r < rows ? uint32_t(M.b[r * M.S + k + s]) : 0u) * p.bsj_block_bytes;
     }
+    if (p.tail_status != nullptr) {  // RrefParams::tail_status: the marker scan's answer from the payload tail
+        int32_t st = RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;
+        int64_t len = 0;
+        int32_t need = 0;
+        if (rows == k) {
+            // lane l: dword l of decoded row k - 1's last 256 bytes = Σ_j T[k-1][j] · (piece j's data dword there)
+            const int64_t L = p.tail_L;
+            const uint8_t *tb = p.pieces + int64_t(o) * p.obj_stride + k + (L - 256) + 4 * lane;
+            uint32_t acc = 0;
+            for (int j0 = 0; j0 < m; j0 += 8) {
+                uint32_t c[8], x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {  // loads of 8 pieces in flight (c is uniform: so is the branch)
+                    const int j = j0 + u;
+                    c[u] = j < m ? uint32_t(M.b[(k - 1) * M.S + k + j]) : 0u;
+                    x[u] = c[u] != 0 ? *reinterpret_cast<const uint32_t *>(tb + int64_t(j) * p.piece_stride) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc ^= mul4(tab, c[u], x[u]);
+            }
+            const uint64_t nz = __ballot(acc != 0);
+            if (nz != 0) {
+                const int h = __builtin_amdgcn_readfirstlane(63 - __builtin_clzll(nz));  // the last lane with a byte
+                const uint32_t a = __builtin_amdgcn_readlane(acc, h);
+                const int b = (31 - __builtin_clz(a)) / 8;
+                const int64_t pos = int64_t(k - 1) * L + (L - 256) + 4 * h + b;
+                const bool ok = ((a >> (8 * b)) & 0xFFu) == kBoundaryMarker && pos > 0;
+                st = ok ? RLNC_OK : RLNC_ERR_INVALID_DECODED_DATA_FORMAT;
+                len = ok ? pos : 0;
+            } else {
+                st = RLNC_OK;  // decided by the product's workgroup (scan_need)
+                need = 1;
+            }
+        }
+        if (lane == 0) {
+            p.tail_status[o] = st;
+            p.tail_len[o] = len;
+            p.tail_need[o] = need;
+        }
+    }
     if constexpr (PROF) {
         ts[4] = wall_clock64();
         ts[5] |= uint64_t(__smid()) << 32;

@@ -1,0 +1,18 @@
+# round-5: the marker scan answered by the small-object elimination from the payload tail (+ the product's workgroups
+# for all-zero tails): full GPU suite, then configs[0] decode A/B against RLNC_FUSED_SCAN=0, interleaved
+set -o pipefail
+O=${1:-gpurun_out/r05_tail}
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+tail -1 $O/gpu_tests.log
+for i in 1 2 3; do
+  r=$(CONFIGS=0 timeout -k 10 120 python scripts/bench_configs.py 2>/dev/null) || exit 1
+  echo "{\"fused\": 1, \"r\": $r}" >> $O/ab.jsonl
+  r=$(RLNC_FUSED_SCAN=0 CONFIGS=0 timeout -k 10 120 python scripts/bench_configs.py 2>/dev/null) || exit 1
+  echo "{\"fused\": 0, \"r\": $r}" >> $O/ab.jsonl
+done
+python3 -c "
+import json
+for l in open('$O/ab.jsonl'):
+    j=json.loads(l); r=j['r']; print('fused', j['fused'], 'decode', r['decode_ms'], 'encode', r['encode_ms'], r['verified'])
+"
