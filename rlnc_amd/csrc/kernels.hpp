@@ -181,9 +181,9 @@ struct RrefParams {
     uint32_t *bsj_stream = nullptr;
     uint32_t bsj_block_bytes = 0;
     int bsj_tile_rows = 0;
-    // optional, with bsj_stream (same kernel): get_final_data_len (decoder.rs:162-177) decided from the last 256
-    // payload bytes -- decoded row k - 1's last 256 bytes computed from T and the pieces' tails (tail_L = L, a multiple
-    // of 4, >= 256; k a multiple of 4): tail_status / tail_len the object's status and final length when its last
+    // optional, with bsj_stream (same kernel): get_final_data_len (decoder.rs:162-177) decided from the last 64
+    // payload bytes -- decoded row k - 1's last 64 bytes computed from T and the pieces' tails (tail_L = L, a multiple
+    // of 4, >= 64; k and the object stride multiples of 4): tail_status / tail_len the object's status and final length when its last
     // nonzero byte lies there (or rank < k), else tail_need[o] = 1 (the product's workgroup scans the whole payload,
     // MatmulParams::scan_need)
     int32_t *tail_status = nullptr;

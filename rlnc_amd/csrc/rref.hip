@@ -152,7 +152,8 @@ static hipError_t launch_rref_one(const RrefParams &p, hipStream_t s, bool *bsj_
         const bool g8 = rref_row_dwords(p.k, p.m) <= 8;
         auto kern = g8 ? &gf_rref_small_kernel<kSmallNW, 8, 2> : &gf_rref_small_kernel<1, 4, 4>;
         int nw = g8 ? kSmallNW : 1;
-        const size_t lds_small = size_t(kTabEntries) * kTabDw * 4 + nw * rref_small_wave_bytes(p.k, p.m);
+        const size_t lds_small = size_t(kTabEntries) * kTabDw * 4 + nw * rref_small_wave_bytes(p.k, p.m) +
+                                 (p.tail_status != nullptr ? nw * rref_small_tail_bytes(p.m) : 0);
         hipLaunchKernelGGL(kern, dim3((p.n_obj + nw - 1) / nw), dim3(64 * nw), lds_small, s, p);
         const hipError_t e = hipGetLastError();
         if (e == hipSuccess && bsj_written) *bsj_written = p.bsj_stream != nullptr && p.bsj_tile_rows > 0;

@@ -19,7 +19,11 @@ static hipError_t launch_rref_one_ab(const RrefParams &p, hipStream_t s);
 // for up to k = 64), the 16-piece blocks of the blocked run (RLNC_BLK = 16) and the small-object knobs
 // (RLNC_SMALL_MIN, RLNC_SMALL_NW).
 bool launch_rref_ab(const RrefParams &p, hipStream_t s, hipError_t *result) {
-    *result = launch_rref_one_ab(p, s);
+    // never the payload-tail answer (RrefParams::tail_status): launch_rref_batch reports no block-offset stream written
+    // from here, so the product never relies on it and the scan kernel answers every object
+    RrefParams q = p;
+    q.tail_status = nullptr;
+    *result = launch_rref_one_ab(q, s);
     return true;
 }
 

@@ -881,6 +881,10 @@ __global__ __launch_bounds__(64 * NW) void gf_rref_batch_kernel(RrefParams p, in
 // resident at once.  Per wave the same steps as gf_rref_batch_kernel<4, 8, 1> (register clean run, the reference's
 // rref verbatim when the clean state ends), with wave-local synchronisation only: after the table copy no wave
 // waits for another.
+// the payload-tail staging of one object (RrefParams::tail_status): the last 64 data bytes of each of its m pieces,
+// moved into LDS by DMA at the kernel's start (a valid payload's marker lies in its last k <= 16 bytes)
+constexpr int kTailBytes = 64;
+__host__ __device__ inline size_t rref_small_tail_bytes(int m) { return size_t(m) * kTailBytes; }
 __host__ __device__ inline size_t rref_small_wave_bytes(int k, int m) {
     return size_t(k + 1) * 4 * size_t(rref_row_dwords(k, m)) + 4 * ((size_t(m) + 3) & ~size_t(3)) +
            ((size_t(m) * k + 15) & ~size_t(15));
@@ -1100,6 +1104,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 
             if (u < k) H[lane * k + u] = hb[u];
     }
     for (int w = lane; w < (k + 1) * M.D; w += 64) M.w[w] = 0;
+    // RrefParams::tail_status: the pieces' last 64 data bytes on their way into this wave's LDS (DMA, no registers;
+    // lanes 0-15, a dword each), used once the elimination is done
+    uint32_t *tailb = lds + kTabEntries * kTabDw + NW * (rref_small_wave_bytes(k, m) / 4) +
+                      size_t(wave) * (rref_small_tail_bytes(m) / 4);
+    if (p.tail_status != nullptr && o < p.n_obj && lane < kTailBytes / 4) {
+        typedef __attribute__((address_space(1))) void gvoid;
+        typedef __attribute__((address_space(3))) void lvoid;
+        const uint8_t *tb = p.pieces + int64_t(o) * p.obj_stride + k + (p.tail_L - kTailBytes) + 4 * lane;
+        for (int j = 0; j < m; ++j)
+            __builtin_amdgcn_global_load_lds((gvoid *)(tb + int64_t(j) * p.piece_stride), (lvoid *)(tailb + (kTailBytes / 4) * j), 4, 0,
+                                             0);
+    }
     __syncthreads();  // the only workgroup barrier: the table, and this wave's headers and zeroed matrix
     if constexpr (PROF) ts[1] = ts[2] = wall_clock64();
     if (o >= p.n_obj) return;
@@ -1135,9 +1151,52 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 
     }
     if (clean) regs_to_lds<G, RT, false>(M, v, rows);
     rsync<false>();
+    // RrefParams::tail_status: the marker scan's answer from the payload tail -- before this wave's stores below, so
+    // that the wait for the staging DMAs does not wait for them too
+    int32_t tail_st = RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;
+    int64_t tail_len = 0;
+    int32_t tail_need = 0;
+    if (p.tail_status != nullptr) {
+        if (rows == k) {
+            // lane l < 16: dword l of decoded row k - 1's last 64 bytes = Σ_j T[k-1][j] · (piece j's data dword
+            // there, staged in LDS at the start)
+            const int64_t L = p.tail_L;
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staging DMAs (long landed)
+            uint32_t acc = 0;
+            for (int j0 = 0; j0 < m; j0 += 8) {
+                uint32_t c[8], x[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int j = j0 + u;
+                    c[u] = j < m ? uint32_t(M.b[(k - 1) * M.S + k + j]) : 0u;
+                    x[u] = j < m && lane < kTailBytes / 4 ? tailb[(kTailBytes / 4) * j + lane] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc ^= mul4(tab, c[u], x[u]);
+            }
+            const uint64_t nz = __ballot(acc != 0);
+            if (nz != 0) {
+                const int h = __builtin_amdgcn_readfirstlane(63 - __builtin_clzll(nz));  // the last lane with a byte
+                const uint32_t a = __builtin_amdgcn_readlane(acc, h);
+                const int b = (31 - __builtin_clz(a)) / 8;
+                const int64_t pos = int64_t(k - 1) * L + (L - kTailBytes) + 4 * h + b;
+                const bool ok = ((a >> (8 * b)) & 0xFFu) == kBoundaryMarker && pos > 0;
+                tail_st = ok ? RLNC_OK : RLNC_ERR_INVALID_DECODED_DATA_FORMAT;
+                tail_len = ok ? pos : 0;
+            } else {
+                tail_st = RLNC_OK;  // decided by the product's workgroup (scan_need)
+                tail_need = 1;
+            }
+        }
+    }
     if constexpr (PROF) ts[3] = wall_clock64();
     for (int pc = lane; pc < m; pc += 64) p.status[int64_t(o) * m + pc] = St[pc];
     if (lane == 0) p.rank[o] = rows;
+    if (p.tail_status != nullptr && lane == 0) {
+        p.tail_status[o] = tail_st;
+        p.tail_len[o] = tail_len;
+        p.tail_need[o] = tail_need;
+    }
     // T row by row, lane = column (m <= 64 here): no per-element index division
     uint8_t *T = p.T + int64_t(o) * p.T_obj;
     for (int r = 0; r < k; ++r)
@@ -1148,46 +1207,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(G == 8 
         const int r = lane & (tr - 1), step = 64 / tr;
         for (int s = lane / tr; s < m; s += step)
             st[s * tr + r] = (r < rows ? uint32_t(M.b[r * M.S + k + s]) : 0u) * p.bsj_block_bytes;
-    }
-    if (p.tail_status != nullptr) {  // RrefParams::tail_status: the marker scan's answer from the payload tail
-        int32_t st = RLNC_ERR_NOT_ALL_PIECES_RECEIVED_YET;
-        int64_t len = 0;
-        int32_t need = 0;
-        if (rows == k) {
-            // lane l: dword l of decoded row k - 1's last 256 bytes = Σ_j T[k-1][j] · (piece j's data dword there)
-            const int64_t L = p.tail_L;
-            const uint8_t *tb = p.pieces + int64_t(o) * p.obj_stride + k + (L - 256) + 4 * lane;
-            uint32_t acc = 0;
-            for (int j0 = 0; j0 < m; j0 += 8) {
-                uint32_t c[8], x[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {  // loads of 8 pieces in flight (c is uniform: so is the branch)
-                    const int j = j0 + u;
-                    c[u] = j < m ? uint32_t(M.b[(k - 1) * M.S + k + j]) : 0u;
-                    x[u] = c[u] != 0 ? *reinterpret_cast<const uint32_t *>(tb + int64_t(j) * p.piece_stride) : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) acc ^= mul4(tab, c[u], x[u]);
-            }
-            const uint64_t nz = __ballot(acc != 0);
-            if (nz != 0) {
-                const int h = __builtin_amdgcn_readfirstlane(63 - __builtin_clzll(nz));  // the last lane with a byte
-                const uint32_t a = __builtin_amdgcn_readlane(acc, h);
-                const int b = (31 - __builtin_clz(a)) / 8;
-                const int64_t pos = int64_t(k - 1) * L + (L - 256) + 4 * h + b;
-                const bool ok = ((a >> (8 * b)) & 0xFFu) == kBoundaryMarker && pos > 0;
-                st = ok ? RLNC_OK : RLNC_ERR_INVALID_DECODED_DATA_FORMAT;
-                len = ok ? pos : 0;
-            } else {
-                st = RLNC_OK;  // decided by the product's workgroup (scan_need)
-                need = 1;
-            }
-        }
-        if (lane == 0) {
-            p.tail_status[o] = st;
-            p.tail_len[o] = len;
-            p.tail_need[o] = need;
-        }
     }
     if constexpr (PROF) {
         ts[4] = wall_clock64();
