@@ -1,7 +1,7 @@
 # round-5 closing measurements: both GPU suites, smoke, the default bench line, a rocprofv3 kernel trace of the same
 # command with the breakdown launches selected, every config, an object-API grid run
 set -o pipefail
-O=gpurun_out/r05_final
+O=${1:-gpurun_out/r05_final}
 mkdir -p $O
 R=$PWD
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
