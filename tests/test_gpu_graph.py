@@ -178,3 +178,59 @@ def test_descriptor_tables_survive_other_eager_calls_before_replay(warm_pad, ext
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "tables ok" in r.stdout
+
+
+def test_small_object_decode_under_graph_capture():
+    """configs[0]'s decode form under capture: the small-object elimination answering the marker scan from the
+    payload tail (RrefParams::tail_status) and the product's workgroups scanning the all-zero tails
+    (MatmulParams::scan_need) -- captured after an eager warm-up, replayed into zeroed outputs, equal to the eager
+    decode, which is checked against the source."""
+    import numpy as np
+    import torch
+
+    import rlnc_amd
+    from rlnc_amd import batch
+
+    ctx = rlnc_amd.Context(0)
+    rng = np.random.default_rng(9)
+    B, k, L = 2048, 16, 4096
+    src = rng.integers(0, 256, (B, k * L), dtype=np.uint8)
+    src[0::3, -1] = 0x81  # marker last: decided by the tail
+    src[1::3, 200:] = 0   # marker early, a long zero tail: scanned by the product's workgroup
+    src[1::3, 199] = 0x81
+    src_d = torch.from_numpy(src.reshape(B, k, L)).cuda()
+    co = torch.from_numpy(rng.integers(0, 256, (B, k, k), dtype=np.uint8)).cuda()
+    pieces = torch.empty((B, k, k + L), dtype=torch.uint8, device="cuda")
+    batch.encode_batch(src_d, co, pieces, ctx)
+
+    def outputs():
+        return (torch.zeros((B, k, L), dtype=torch.uint8, device="cuda"),
+                torch.full((B, k), -1, dtype=torch.int32, device="cuda"),
+                torch.full((B,), -1, dtype=torch.int32, device="cuda"),
+                torch.full((B,), -1, dtype=torch.int64, device="cuda"))
+
+    eager = outputs()
+    batch.decode_batch_device(pieces, k, *eager, ctx)  # also the warm-up: workspaces grow here
+    torch.cuda.synchronize()
+    cap = outputs()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            batch.decode_batch_device(pieces, k, *cap, ctx)
+    for t in cap:
+        t.fill_(0)
+    g.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(cap, eager):
+        assert torch.equal(a, b)
+    ost, dl = eager[2].cpu().numpy(), eager[3].cpu().numpy()
+    full = (eager[1] == 0).sum(1).cpu().numpy() == k
+    dec = eager[0].cpu().numpy().reshape(B, k * L)
+    assert full.sum() > B * 0.9
+    for o in np.nonzero(full)[0]:
+        assert np.array_equal(dec[o], src[o]), o
+        if o % 3 == 0:
+            assert ost[o] == 0 and dl[o] == k * L - 1, o
+        elif o % 3 == 1:
+            assert ost[o] == 0 and dl[o] == 199, o
