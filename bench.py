@@ -451,7 +451,11 @@ def run_gpu(args, dist: Dist):
     import numpy as np
     import torch
 
-    torch.cuda.set_device(dist.local_rank)
+    # the rank's device, chosen here in the fresh rank process (the spawning parent never touches the GPU): local
+    # rank modulo the devices this process sees, so N ranks on a box with fewer GPUs share them (two ranks on the one
+    # GPU of a test lease: tests/test_gpu_multirank.py); one rank per GPU on a full node
+    device = dist.local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     dist.init()
 
     import rlnc_amd
@@ -465,9 +469,9 @@ def run_gpu(args, dist: Dist):
         objs = args.objects // dist.world + (1 if dist.rank < args.objects % dist.world else 0)
     C = min(args.chunk, objs)  # objects per launch
     chunks = [(c0, min(objs, c0 + C)) for c0 in range(0, objs, C)]
-    ctx = rlnc_amd.Context(dist.local_rank)
+    ctx = rlnc_amd.Context(device)
     ctx.set_kernel_variant(args.variant, args.tile_rows)
-    dev = torch.device("cuda", dist.local_rank)
+    dev = torch.device("cuda", device)
 
     # synthetic objects of the named shape, generated on device; coefficients from a host RNG (like
     # rng.fill_bytes in the reference) and uploaded before timing
@@ -490,8 +494,8 @@ def run_gpu(args, dist: Dist):
                     obj=(0, 0))
 
     sets = [buffers(C)]
-    enc_events, dec_events = [], []
-    ctx_side = rlnc_amd.Context(dist.local_rank) if args.pipeline else None
+    enc_events, dec_events, apply_events, plan_events = [], [], [], []
+    ctx_side = rlnc_amd.Context(device) if args.pipeline else None
     if ctx_side is not None:
         ctx_side.set_kernel_variant(args.variant, args.tile_rows)  # the plan is laid out for the launch's variant
     side = torch.cuda.Stream(dev) if args.pipeline else None
@@ -508,7 +512,7 @@ def run_gpu(args, dist: Dist):
     def launch_serial(c0, c1, S):
         s_, co, pieces, decoded, pst, ost, dl, T, rank = views(S, c0, c1)
         received = pieces[:, :m]
-        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0, e1, ea, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
         if args.pipeline:
             # side stream: the encode's code-block address stream, the coded pieces' headers (bytes 0..k of each
             # piece), then the elimination over them; launch stream: the data bytes k.. of the same pieces (disjoint
@@ -518,7 +522,12 @@ def run_gpu(args, dist: Dist):
             with torch.cuda.stream(side):
                 side.wait_event(ev_start)
                 if not args.no_plan:
+                    # the address stream's own launch, timed on the side stream it runs on (outside e0..e1)
+                    p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    p0.record()
                     batch.encode_batch_prepare(s_, co, pieces, S["plan"], ctx_side)
+                    p1.record()
+                    plan_events.append((p0, p1))
                 ev_plan.record()
                 batch.encode_batch_headers(co, pieces, ctx_side)
                 if not args.encode_only:
@@ -539,7 +548,9 @@ def run_gpu(args, dist: Dist):
         if not args.encode_only:
             if args.pipeline:
                 torch.cuda.current_stream().wait_event(ev_elim)
+                ea.record()  # the decode's data side alone: T x data (+ its address launch and the marker scan)
                 batch.decode_batch_apply(received, k, T, rank, decoded, ost, dl, ctx)
+                apply_events.append((ea, e2))
             else:
                 batch.decode_batch_device(received, k, decoded, pst, ost, dl, ctx)
         e2.record()
@@ -558,7 +569,7 @@ def run_gpu(args, dist: Dist):
     pipelined = args.pipeline == 2 and not args.encode_only
     if pipelined:
         sets.append(buffers(C))
-        ctx_dec = rlnc_amd.Context(dist.local_rank)
+        ctx_dec = rlnc_amd.Context(device)
         ctx_dec.set_kernel_variant(args.variant, args.tile_rows)
         s_dec = torch.cuda.Stream(dev)
         ev_done = [torch.cuda.Event(), torch.cuda.Event()]
@@ -651,6 +662,13 @@ def run_gpu(args, dist: Dist):
     enc_ms = sum(a.elapsed_time(b) for a, b in timed_enc) / len(timed_enc)
     timed_dec = dec_events[skip:] or dec_events
     dec_ms = sum(a.elapsed_time(b) for a, b in timed_dec) / len(timed_dec)
+
+    def mean_ms(evs):
+        evs = evs[skip:] or evs
+        return sum(a.elapsed_time(b) for a, b in evs) / len(evs) if evs else None
+
+    apply_ms = mean_ms(apply_events)  # pipeline-1 groups only (launch_serial with --pipeline >= 1)
+    plan_ms = mean_ms(plan_events)
     ok_rank = dist.allgather(float(ok))
     ok = all(v == 1.0 for v in ok_rank)
     enc_ms_rank = dist.allgather(enc_ms)
@@ -672,6 +690,8 @@ def run_gpu(args, dist: Dist):
     enc_compulsory = B * (k * L + n * (k + L))       # source read once + coded pieces written
     variant = VARIANTS[args.variant]
     traffic, traffic_src = pmc_traffic(variant, B, k, L, n)
+    # the product kernel alone is inside e0..e1 unless --no-plan puts the address launch in front of it
+    enc_kernel = KERNELS[variant] if args.no_plan else KERNELS[variant].replace("bsj_offset_kernel + ", "")
     ceiling = None if args.no_ceiling else xor3_ceiling()
     live = ceiling["peak_T_ma_per_s"] if ceiling else None
     roofline = {
@@ -682,14 +702,18 @@ def run_gpu(args, dist: Dist):
         "peak": round(SPEC_PEAK_T_MA, 2),
         "unit": "T GF(2^8) multiply-adds/s",
         "frac": round(achieved / SPEC_PEAK_T_MA, 4),
+        "frac_definition": "achieved / peak, peak = the guide's VALU issue rate (since round 5; rounds 1-4 reported "
+                           "frac against the live XOR3 ceiling, which is frac_live now)",
         # beside it, the live XOR3-issue ceiling measured in this run (measure/gf_ceiling.hip: independent XOR3s only,
         # 0.75-0.77 of the spec rate -- the clock under load and three-source issue)
         "peak_live": live,
         "frac_live": round(achieved / live, 4) if live else None,
         "traffic": traffic,
         "traffic_source": traffic_src,
-        "kernel": f"{KERNELS[variant]} (encode: {n} coded pieces x {B} objects per launch)",
+        "kernel": f"{enc_kernel} (encode: {n} coded pieces x {B} objects per launch)",
         "kernel_ms": round(enc_ms, 4),
+        # the code-block address launch (rlnc_encode_batch_prepare) on the side stream, outside kernel_ms
+        "address_stream_ms": round(plan_ms, 4) if plan_ms is not None else None,
         "kernel_ms_how": ("HIP events around the encode launch on its stream, in pipeline-1 launch groups (the "
                           "elimination beside it, no other group's kernels)") if args.pipeline else
                          "HIP events around the encode launch",
@@ -704,6 +728,37 @@ def run_gpu(args, dist: Dist):
                        "note": "the reference's encoder byte counter charges the source once per coded piece; "
                                f"{n} coded pieces share one source pass, so this is not a bandwidth"},
     }
+
+    # the decode's data side (its own roofline): decoded rows = T (k x m) x the m received pieces' data,
+    # k * m * L multiply-adds per object in the same bit-sliced engine (32-row tiles: the 4-wave shared program), timed
+    # with HIP events on its stream around rlnc_decode_batch_apply in the pipeline-1 groups (after the wait for the
+    # elimination, so only the apply's launches: its address launch, the product and the marker scan)
+    roofline_decode = None
+    if apply_ms:
+        ma_dec = B * k * m * L
+        dec_achieved = ma_dec / (apply_ms * 1e-3) / 1e12
+        dec_compulsory = B * (m * L + k * L)  # received data read once + decoded rows written
+        dtraffic, dtraffic_src = pmc_traffic("decode:" + variant, B, k, L, n)
+        roofline_decode = {
+            "bound": "valu",
+            "achieved": round(dec_achieved, 2),
+            "peak": round(SPEC_PEAK_T_MA, 2),
+            "unit": "T GF(2^8) multiply-adds/s",
+            "frac": round(dec_achieved / SPEC_PEAK_T_MA, 4),
+            "frac_live": round(dec_achieved / live, 4) if live else None,
+            "traffic": dtraffic,
+            "traffic_source": dtraffic_src,
+            "kernel": (f"bsj_offset_kernel + gf_matmul_bsj_kernel<4, true> + final_len_scan_kernel (decode data side: "
+                       f"{k} decoded rows from {m} received pieces x {B} objects per launch)"),
+            "kernel_ms": round(apply_ms, 4),
+            "kernel_ms_how": "HIP events on the decode's stream around rlnc_decode_batch_apply (after its wait for the "
+                             "elimination), in pipeline-1 launch groups",
+            "multiply_adds_per_launch": ma_dec,
+            "hbm": {"compulsory_bytes": dec_compulsory,
+                    "compulsory_GBps": round(dec_compulsory / (apply_ms * 1e-3) / 1e9, 1),
+                    "compulsory_frac": round(dec_compulsory / (apply_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "traffic_over_compulsory": round(dtraffic / dec_compulsory, 4) if dtraffic else None},
+        }
 
     # supplementary HBM roofline: the same source, ONE coded piece per object per launch (configs[1]'s encode
     # at one output row, ~1 multiply-add per source byte: the HBM-bound form of the north star's "encode at
@@ -753,7 +808,8 @@ def run_gpu(args, dist: Dist):
         "decode_ms_per_rank": [round(v, 4) for v in dec_ms_rank],
         # 1: the device runs 16-byte vector memory instructions at any byte address (probed at context creation;
         # misaligned rows take the vector kernels directly), 0: they go through realigning copies
-        "unaligned_vector_access": int(ctx.lib.rlnc_device_unaligned_vector_access(dist.local_rank)),
+        "unaligned_vector_access": int(ctx.lib.rlnc_device_unaligned_vector_access(device)),
+        "device_per_rank": [int(v) for v in dist.allgather(float(device))],
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4),
@@ -780,11 +836,13 @@ def run_gpu(args, dist: Dist):
                             "i's decode (two buffer sets)"}[args.pipeline],
         },
         "roofline": roofline,
+        "roofline_decode": roofline_decode,
         "hbm_single_pass_encode": single,
         "cpu_baseline": None,
         "breakdown": {
             "encode_kernel_ms": round(enc_ms, 4),
             "decode_ms": round(dec_ms, 4),
+            "decode_apply_ms": round(apply_ms, 4) if apply_ms is not None else None,
             "encode_T_ma_per_s": round(achieved, 2),
             "encode_GiBps_refcounter": round(B * n * encode_counter(k, L) / (enc_ms * 1e-3) / GIB, 1),
             "decode_GiBps_refcounter": round(B * decode_counter(k, L) / (dec_ms * 1e-3) / GIB, 2) if dec_ms else None,

@@ -18,6 +18,8 @@
 #include <utility>
 #include <vector>
 
+#include <sys/mman.h>
+
 #include "../rlnc_hip.h"
 
 namespace rlnc {
@@ -136,6 +138,18 @@ struct ZeroedAlloc {
 };
 
 using ZBytes = std::vector<uint8_t, ZeroedAlloc<uint8_t>>;
+
+// A fresh result buffer this mirror allocated (get_decoded_data's Bytes) of >= 8 MiB: its whole 2 MiB-aligned pages
+// may be backed by transparent huge pages (MADV_HUGEPAGE, a hint where the host's THP mode is "madvise"), so the
+// library's parallel copy-out faults it in 2 MiB at a time (32 MiB rows 2.4-3.8 -> 1.7-2.3 ms).  The
+// library itself does not advise memory it does not own (unless RLNC_COPY_HUGEPAGE=1).
+inline void advise_huge_pages(void *p, size_t n) {
+    if (n < (size_t(8) << 20)) return;
+    constexpr uintptr_t kHuge = uintptr_t(2) << 20;
+    const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
+    const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + n) & ~(kHuge - 1);
+    if (b > a) (void)madvise(reinterpret_cast<void *>(a), b - a, MADV_HUGEPAGE);
+}
 inline bool operator==(const ZBytes &a, const std::vector<uint8_t> &b) {
     return a.size() == b.size() && std::equal(a.begin(), a.end(), b.begin());
 }
@@ -247,9 +261,13 @@ class Decoder {
     size_t get_remaining_piece_count() const { return rlnc_decoder_get_remaining_piece_count(h_.h); }
     Result<Bytes> get_decoded_data() {  // decoder.rs:136-159
         Bytes out(get_num_pieces_coded_together() * get_piece_byte_len());
+        detail::advise_huge_pages(out.data(), out.size());
         size_t n = 0;
         auto r = detail::status(rlnc_decoder_get_decoded_data(h_.h, out.data(), out.size(), &n));
         if (r.is_err()) return r.error();
+        // out[n] holds the boundary marker and every byte after it is zero: clear the marker so that a later
+        // resize(m > n) of the result regrows into zeros, as the crate's Vec does
+        if (n < out.size()) out[n] = 0;
         out.resize(n);
         return out;
     }

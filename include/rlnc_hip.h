@@ -83,6 +83,10 @@ int rlnc_context_use_own_stream(rlnc_context *ctx);
 void *rlnc_context_get_stream(rlnc_context *ctx);
 int rlnc_context_synchronize(rlnc_context *ctx);
 int rlnc_context_device(const rlnc_context *ctx);
+/* *capturing = 1 when `hip_stream` (NULL: the null stream) is inside a HIP stream capture, else 0, asked of the HIP
+ * runtime this library is linked against (the one a host framework such as torch shares).  On any runtime error it
+ * returns RLNC_ERR_DEVICE and sets *capturing = 1 (a caller deciding whether it may synchronise assumes the worst). */
+int rlnc_stream_is_capturing(void *hip_stream, int *capturing);
 /* 1 when 16-byte vector loads/stores (and LDS-DMA) at any byte address return the right bytes on `device` (the
  * queue's unaligned memory mode, checked by a probe kernel when the first context on the device is created):
  * piece rows at any alignment (odd L from Encoder::new, data at byte k of a (k + L)-byte coded piece) then take the
@@ -239,9 +243,14 @@ int rlnc_encode_batch_data(rlnc_context *ctx, const uint8_t *src_dev, size_t k, 
  * the (coefficient-only) address launch on ITS context's stream into plan_dev (device memory of at least
  * rlnc_encode_batch_plan_bytes bytes), e.g. on a side stream beside other work; _data_planned, with the same
  * arguments and the same kernel variant, then runs the product without that launch (the caller orders it after the
- * prepare, e.g. with an event).  A plan buffer serves the product it was prepared for (same buffers, shape, device,
- * variant; the coefficients as they were at the prepare); _data_planned returns InvalidArgument for any other.
- * Writes exactly what rlnc_encode_batch_data writes. */
+ * prepare, e.g. with an event).  A plan buffer serves the product it was prepared for.  The library remembers each
+ * prepare by the plan buffer's address with its arguments (buffers, shape, device, kernel variant) and
+ * _data_planned returns InvalidArgument when those arguments differ.  What it cannot see is the memory itself: the
+ * caller keeps the plan buffer alive and unwritten, and the coefficient bytes unchanged, from the prepare to the
+ * product.  A plan buffer freed and reallocated at the same address, or coefficients rewritten in place, must be
+ * prepared again: the product takes the buffer's entries as code addresses, so a stale plan gives wrong bytes and
+ * a plan buffer overwritten with other data is undefined behaviour, like a dangling pointer.  Writes exactly what
+ * rlnc_encode_batch_data writes. */
 size_t rlnc_encode_batch_plan_bytes(size_t k, size_t num_objects, size_t n);
 int rlnc_encode_batch_prepare(rlnc_context *ctx, const uint8_t *src_dev, size_t k, size_t L, size_t num_objects,
                               const uint8_t *coeffs_dev, size_t n, uint8_t *pieces_dev, void *plan_dev,

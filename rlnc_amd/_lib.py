@@ -64,6 +64,7 @@ _SIGS = {
     "rlnc_context_synchronize": (C.c_int, [vp]),
     "rlnc_context_device": (C.c_int, [vp]),
     "rlnc_device_unaligned_vector_access": (C.c_int, [C.c_int]),
+    "rlnc_stream_is_capturing": (C.c_int, [vp, C.POINTER(C.c_int)]),
     "rlnc_gf256_inplace_mul_vec_by_scalar": (C.c_int, [vp, vp, C.c_size_t, C.c_uint8]),
     "rlnc_gf256_inplace_add_vectors": (C.c_int, [vp, vp, vp, C.c_size_t]),
     "rlnc_gf256_mul_vec_by_scalar_then_add_into_vec": (C.c_int, [vp, vp, vp, C.c_size_t, C.c_uint8]),

@@ -118,25 +118,18 @@ def _capturing() -> bool:
         return False
 
 
-_hip = None
-
-
 def _stream_capturing(stream_handle: int) -> bool:
-    """hipStreamIsCapturing on a raw stream handle (the HIP runtime torch has loaded); True when unsure."""
-    global _hip
+    """hipStreamIsCapturing on a raw stream handle, asked through librlnc_hip (rlnc_stream_is_capturing: the HIP
+    runtime the library -- and torch -- has loaded, so the handle means the same stream); True when unsure."""
     import ctypes
 
     try:
-        if _hip is None:
-            _hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
-            _hip.hipStreamIsCapturing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
-            _hip.hipStreamIsCapturing.restype = ctypes.c_int
-        st = ctypes.c_int(0)
-        if _hip.hipStreamIsCapturing(ctypes.c_void_p(stream_handle or None), ctypes.byref(st)) != 0:
+        st = ctypes.c_int(1)
+        if _lib.load().rlnc_stream_is_capturing(ctypes.c_void_p(stream_handle or None), ctypes.byref(st)) != 0:
             return True
-        return st.value != 0  # hipStreamCaptureStatusNone = 0
-    except OSError:
-        return False
+        return st.value != 0
+    except Exception:
+        return True
 
 
 def release_stream_contexts() -> None:

@@ -423,6 +423,17 @@ void *rlnc_context_get_stream(rlnc_context *ctx) { return ctx ? ctx->stream : nu
 int rlnc_context_device(const rlnc_context *ctx) { return ctx ? ctx->device : -1; }
 int rlnc_device_unaligned_vector_access(int device) { return rlnc::unaligned_vector_access(device); }
 
+int rlnc_stream_is_capturing(void *hip_stream, int *capturing) {
+    CHECK_ARG(capturing != nullptr);
+    *capturing = 1;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const hipError_t e = hipStreamIsCapturing(static_cast<hipStream_t>(hip_stream), &cs);
+    if (e != hipSuccess)
+        return set_error(RLNC_ERR_DEVICE, "hipStreamIsCapturing: %s", hipGetErrorString(e));
+    *capturing = cs != hipStreamCaptureStatusNone;
+    return RLNC_OK;
+}
+
 int rlnc_context_synchronize(rlnc_context *ctx) {
     CHECK_ARG(ctx != nullptr);
     HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -1010,12 +1021,15 @@ struct CopyTrace {
 CopyTrace g_copy_trace;
 
 // The whole 2 MiB-aligned pages inside dst[0, n) may be backed by transparent huge pages (a hint, where the host's
-// THP mode is "madvise"): a fresh buffer then faults in 2 MiB at a time instead of 4 KiB.  Only pages that lie entirely
-// inside the caller's output buffer are advised.  RLNC_COPY_HUGEPAGE=0 (A/B knob, read once) turns it off.
+// THP mode is "madvise"): a fresh buffer then faults in 2 MiB at a time instead of 4 KiB.  The advice changes the
+// flags of the caller's mapping (they outlive the buffer in its allocator's arena), so the library gives it only when
+// the caller opts in with RLNC_COPY_HUGEPAGE=1 (read once).  A caller that owns a fresh result buffer advises it
+// itself: the C++ mirror's get_decoded_data does (include/rlnc/full.hpp), which is where the 32 MB rows' huge-page
+// gain is measured.
 void advise_huge(uint8_t *dst, size_t n) {
     static const bool on = [] {
         const char *e = getenv("RLNC_COPY_HUGEPAGE");
-        return !e || atoi(e) != 0;
+        return e && atoi(e) != 0;
     }();
     constexpr uintptr_t kHuge = uintptr_t(2) << 20;
     const uintptr_t a = (reinterpret_cast<uintptr_t>(dst) + kHuge - 1) & ~(kHuge - 1);

@@ -16,25 +16,37 @@ namespace {
 constexpr size_t kMinSlice = size_t(1) << 20;  // below this per thread the hand-off costs more than it saves
 constexpr size_t kPage = 4096;
 
+// one store into every 4 KiB page that dst[a, b) intersects
+void touch(uint8_t *dst, size_t a, size_t b) {
+    if (a >= b) return;
+    volatile uint8_t *v = dst;
+    v[a] = 0;
+    for (size_t i = (a + kPage - reinterpret_cast<uintptr_t>(dst + a) % kPage); i < b; i += kPage) v[i] = 0;
+}
+
 // Persistent workers (created on first use, detached: they sleep on the condition variable between copies and die
 // with the process).  One copy at a time; concurrent callers serialise on `call_mu` (a copy of many MiB is
 // bandwidth-bound, two at once would not finish sooner).
 class Pool {
    public:
-    // src == nullptr: touch instead of copy (one zero byte per 4 KiB page of each slice)
+    // src == nullptr: touch instead of copy (one zero byte in each 4 KiB page of each slice)
     void run(uint8_t *dst, const uint8_t *src, size_t n, int threads) {
         std::lock_guard<std::mutex> call(call_mu_);
         ensure(threads - 1);
-        // slices on page boundaries of the destination: no two threads fault the same page
+        // slice boundaries on page boundaries of the destination ADDRESS (dst + offset), whatever dst's alignment:
+        // slice 0 runs to the first page boundary past its share, every later slice starts on one, so no two threads
+        // fault the same page
         const size_t per = ((n + threads - 1) / threads + kPage - 1) & ~(kPage - 1);
+        const size_t lead = (kPage - reinterpret_cast<uintptr_t>(dst) % kPage) % kPage;
         {
             std::lock_guard<std::mutex> lock(mu_);
             dst_ = dst;
             src_ = src;
             n_ = n;
             per_ = per;
+            lead_ = lead;
             next_ = 1;  // slice 0 is the caller's
-            slices_ = (n + per - 1) / per;
+            slices_ = n > lead + per ? (n - lead + per - 1) / per : 1;
             pending_ = slices_ - 1;
         }
         cv_.notify_all();
@@ -52,12 +64,14 @@ class Pool {
     }
 
    private:
+    // slice s = [bound(s), bound(s + 1)): bound(0) = 0, bound(s) = lead + s * per (a page boundary of dst + offset)
+    size_t bound(size_t s) const { return s == 0 ? 0 : std::min(n_, lead_ + s * per_); }
     void copy_slice(size_t s) {
-        const size_t a = s * per_, b = std::min(n_, a + per_);
+        const size_t a = bound(s), b = s + 1 == slices_ ? n_ : bound(s + 1);
         if (src_ != nullptr) {
             std::memcpy(dst_ + a, src_ + a, b - a);
         } else {
-            for (size_t i = a; i < b; i += kPage) reinterpret_cast<volatile uint8_t *>(dst_)[i] = 0;
+            touch(dst_, a, b);
         }
     }
     void ensure(int workers) {
@@ -82,7 +96,7 @@ class Pool {
     size_t workers_ = 0;
     uint8_t *dst_ = nullptr;
     const uint8_t *src_ = nullptr;
-    size_t n_ = 0, per_ = 0, next_ = 0, slices_ = 0, pending_ = 0;
+    size_t n_ = 0, per_ = 0, lead_ = 0, next_ = 0, slices_ = 0, pending_ = 0;
 };
 
 Pool &pool() {
@@ -95,7 +109,7 @@ Pool &pool() {
 void par_touch(void *dst, size_t n, int threads) {
     threads = int(std::min<size_t>(size_t(std::max(1, threads)), n / kMinSlice));
     if (threads <= 1) {
-        for (size_t i = 0; i < n; i += kPage) static_cast<volatile uint8_t *>(dst)[i] = 0;
+        touch(static_cast<uint8_t *>(dst), 0, n);
         return;
     }
     pool().run(static_cast<uint8_t *>(dst), nullptr, n, threads);

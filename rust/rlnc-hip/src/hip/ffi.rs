@@ -135,6 +135,7 @@ unsafe extern "C" {
     pub fn rlnc_context_get_stream(ctx: *mut rlnc_context) -> *mut c_void;
     pub fn rlnc_context_synchronize(ctx: *mut rlnc_context) -> c_int;
     pub fn rlnc_context_device(ctx: *const rlnc_context) -> c_int;
+    pub fn rlnc_stream_is_capturing(hip_stream: *mut c_void, capturing: *mut c_int) -> c_int;
     pub fn rlnc_device_unaligned_vector_access(device: c_int) -> c_int;
 
     // L1 vector primitives, src/common/simd/mod.rs:18-119 (device buffers)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Drives the many-small-objects elimination alone (configs[0] shape: 4,096 objects x k = 16, 16 received pieces)
-REPS times, for rocprofv3 PMC passes (scripts/r05_pmc_elim.sh) and HIP-event timing (printed, median of 5 x 10)."""
+REPS times, for rocprofv3 PMC passes (scripts/archive/r05_pmc_elim.sh) and HIP-event timing (printed, median of 5 x 10)."""
 import json
 import os
 import sys

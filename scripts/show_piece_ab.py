@@ -1,4 +1,4 @@
-"""Summarise gpurun_out/piece_ab.txt (scripts/r04_piece_ab.sh) one line per row."""
+"""Summarise gpurun_out/piece_ab.txt (scripts/archive/r04_piece_ab.sh) one line per row."""
 import json
 import sys
 

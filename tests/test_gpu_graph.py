@@ -234,3 +234,71 @@ def test_small_object_decode_under_graph_capture():
             assert ost[o] == 0 and dl[o] == k * L - 1, o
         elif o % 3 == 1:
             assert ost[o] == 0 and dl[o] == 199, o
+
+
+# stream-context eviction must skip a context whose stream is mid-capture even when the capture is on a
+# stream that is not torch's current one.  The capture status is asked through librlnc_hip (rlnc_stream_is_capturing,
+# the runtime torch shares), and an error counts as capturing.
+CHILD_EVICT = r"""
+import sys
+sys.path.insert(0, ROOT)
+import numpy as np
+import torch
+import rlnc_amd
+from rlnc_amd import batch, context
+
+rng = np.random.default_rng(21)
+B, k, L, n = 2, 8, 4096, 6
+src = torch.from_numpy(rng.integers(0, 256, (B, k, L), dtype=np.uint8)).cuda()
+co = torch.from_numpy(rng.integers(0, 256, (B, n, k), dtype=np.uint8)).cuda()
+ref = torch.zeros((B, n, k + L), dtype=torch.uint8, device="cuda")
+batch.encode_batch(src, co, ref, rlnc_amd.Context(0))
+torch.cuda.synchronize()
+cap_s = torch.cuda.Stream()
+others = [torch.cuda.Stream() for _ in range(context.STREAM_CONTEXTS_PER_THREAD + 2)]
+# the capture stream's context first (least recently used), then enough others to fill the per-thread cap
+for s in [cap_s] + others[:context.STREAM_CONTEXTS_PER_THREAD - 1]:
+    with torch.cuda.stream(s):
+        out = torch.zeros_like(ref)
+        batch.encode_batch(src, co, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+key = (0, cap_s.cuda_stream)
+assert key in context._tls.sctxs
+assert not context._stream_capturing(cap_s.cuda_stream)
+x = torch.zeros(16, device="cuda")
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g, stream=cap_s, capture_error_mode="relaxed"):
+    x.add_(1)  # torch work captured on cap_s; no rlnc call on cap_s, so its context is not graph-bound
+    assert context._stream_capturing(cap_s.cuda_stream)
+    assert torch.cuda.current_stream().cuda_stream == cap_s.cuda_stream
+    # eager rlnc calls on fresh streams (not the current, capturing one): each new stream context overflows the
+    # cap; eviction must pass over cap_s's context (closing it would synchronise a capturing stream)
+    for s in others[context.STREAM_CONTEXTS_PER_THREAD - 1:]:
+        with torch.cuda.stream(s):
+            out = torch.zeros_like(ref)
+            batch.encode_batch(src, co, out)
+        s.synchronize()
+        assert torch.equal(out, ref)
+    assert key in context._tls.sctxs, "the capturing stream's context was evicted"
+    x.add_(1)
+g.replay()
+torch.cuda.synchronize()
+assert torch.equal(x, torch.full_like(x, 2)), x
+assert not context._stream_capturing(cap_s.cuda_stream)
+# outside the capture the next overflow may evict it again
+with torch.cuda.stream(others[0]):
+    out = torch.zeros_like(ref)
+    batch.encode_batch(src, co, out)
+torch.cuda.synchronize()
+assert torch.equal(out, ref)
+assert len(context._tls.sctxs) <= context.STREAM_CONTEXTS_PER_THREAD
+print("evict ok")
+"""
+
+
+def test_stream_context_eviction_skips_capturing_non_current_stream():
+    code = CHILD_EVICT.replace("ROOT", repr(ROOT))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "evict ok" in r.stdout
