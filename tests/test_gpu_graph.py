@@ -274,14 +274,16 @@ with torch.cuda.graph(g, stream=cap_s, capture_error_mode="relaxed"):
     assert torch.cuda.current_stream().cuda_stream == cap_s.cuda_stream
     # eager rlnc calls on fresh streams (not the current, capturing one): each new stream context overflows the
     # cap; eviction must pass over cap_s's context (closing it would synchronise a capturing stream)
+    outs = []
     for s in others[context.STREAM_CONTEXTS_PER_THREAD - 1:]:
         with torch.cuda.stream(s):
-            out = torch.zeros_like(ref)
-            batch.encode_batch(src, co, out)
+            outs.append(torch.zeros_like(ref))
+            batch.encode_batch(src, co, outs[-1])
         s.synchronize()
-        assert torch.equal(out, ref)
     assert key in context._tls.sctxs, "the capturing stream's context was evicted"
     x.add_(1)
+for out in outs:  # compared outside the capture (a comparison on the capturing stream would synchronise it)
+    assert torch.equal(out, ref)
 g.replay()
 torch.cuda.synchronize()
 assert torch.equal(x, torch.full_like(x, 2)), x
