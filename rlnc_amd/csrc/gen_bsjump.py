@@ -65,8 +65,16 @@ def ACC(i, g, p):  # output row i, group g, plane p (the blocks name row 0; M0 a
     return i * 16 + g * 8 + p
 
 
+# --setplanes (experiment, round 6): the shared programs exchange only the 4 transposed planes of a set through LDS
+# (one ds_write_b128 per builder, one ds_read_b128 per set and wave instead of four) and every wave builds the 11
+# composite entries of each set itself (44 VOP2 XORs per source row per wave): a quarter of the LDS read traffic for
+# more VALU.  The planes sit first in each set's 16 registers (a contiguous quad), entry 0 last.
+SETPLANES = False
+SP_POS = {1: 0, 2: 1, 4: 2, 8: 3, 3: 4, 5: 5, 6: 6, 7: 7, 9: 8, 10: 9, 11: 10, 12: 11, 13: 12, 14: 13, 15: 14, 0: 15}
+
+
 def G(g, h, v):  # combination v of half h of group g (G[g][h][0] = 0)
-    return 128 + g * 32 + h * 16 + v
+    return 128 + g * 32 + h * 16 + (SP_POS[v] if SETPLANES else v)
 
 
 def RAW(g, d):  # the current source row's 64 bytes, read from the LDS ring
@@ -422,17 +430,40 @@ def own_set(L, rb, cslot):
     entries by VOP2 XORs, then 4 ds_write_b128 to set slot `cslot` (entry 0 is the zero register)."""
     L += [f"s_cmp_eq_u32 s{S_H}, 0", "s_cbranch_scc0 4f"]
     for h in range(2):
-        planes = {4 * h + b: OWN(1 << b) for b in range(4)}
-        transpose({d: RB(rb, d) for d in range(8)}, planes, L, half=h)
-        L += [f"v_xor_b32 v{OWN(x)}, v{OWN(y)}, v{OWN(z)}" for x, y, z in
-              [(3, 1, 2), (5, 1, 4), (6, 2, 4), (7, 3, 4), (9, 1, 8), (10, 2, 8), (11, 3, 8), (12, 4, 8),
-               (13, 5, 8), (14, 6, 8), (15, 7, 8)]]
+        if SETPLANES:  # the 4 planes only, as one contiguous quad OWN(0..3)
+            planes = {4 * h + b: OWN(b) for b in range(4)}
+            transpose({d: RB(rb, d) for d in range(8)}, planes, L, half=h)
+        else:
+            planes = {4 * h + b: OWN(1 << b) for b in range(4)}
+            transpose({d: RB(rb, d) for d in range(8)}, planes, L, half=h)
+            L += [f"v_xor_b32 v{OWN(x)}, v{OWN(y)}, v{OWN(z)}" for x, y, z in
+                  [(3, 1, 2), (5, 1, 4), (6, 2, 4), (7, 3, 4), (9, 1, 8), (10, 2, 8), (11, 3, 8), (12, 4, 8),
+                   (13, 5, 8), (14, 6, 8), (15, 7, 8)]]
         L.append("s_branch 6f" if h == 0 else "6:")
         if h == 0:
             L.append("4:")
     sfx, base = cslot_addr(cslot)
-    for q in range(4):
+    for q in range(1 if SETPLANES else 4):
         L.append(f"ds_write_b128 %[ldscw{sfx}], v[{OWN(4 * q)}:{OWN(4 * q) + 3}] offset:{base + q * 1024}")
+
+
+def set_reads(L, sfx, base):
+    """The four sets of a source row from LDS: 16 ds_read_b128 (whole sets), or with --setplanes one per set (the
+    planes) into the set's first quad."""
+    for st in range(4):
+        for q in range(1 if SETPLANES else 4):
+            r = G(st >> 1, st & 1, 1) if SETPLANES else G(st >> 1, st & 1, 4 * q)
+            L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsc{sfx}] offset:{base + st * CS_SET + q * 1024}")
+
+
+def set_combos(L):
+    """--setplanes: the 11 composite entries of the four sets from their planes, in every wave."""
+    if SETPLANES:
+        for st in range(4):
+            combos(st >> 1, st & 1, L)
+
+
+SET_WAIT = 6  # LDS ops a builder leaves in flight at the set-read wait: 2 staging reads + 4 set writes
 
 
 def body_s(L, j, cons=False):
@@ -446,10 +477,7 @@ def body_s(L, j, cons=False):
         L.append("s_setprio 0")
     if "sprio2" in DIAG:
         L.append("s_setprio 2")  # experiment: set building (what the other waves wait for next row) first
-    for st in range(4):
-        for q in range(4):
-            r = G(st >> 1, st & 1, 4 * q)
-            L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsc] offset:{(j % 2) * CS_SLOT + st * CS_SET + q * 1024}")
+    set_reads(L, "", (j % 2) * CS_SLOT)
     if cons:
         L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 20f"]
     for hh in range(2):
@@ -468,10 +496,11 @@ def body_s(L, j, cons=False):
         L.append("s_setprio 0")
     L += [
         # the 16 set reads (LDS returns in order; 2 staging reads + 4 writes may fly)
-        "s_waitcnt lgkmcnt(6)" if "snowait" not in DIAG else "s_nop 0",
+        f"s_waitcnt lgkmcnt({SET_WAIT})" if "snowait" not in DIAG else "s_nop 0",
     ]
     if cons:  # consumer waves: no staging reads or set writes in flight, the 16 set reads are the last
         L += ["s_branch 21f", "20:", "s_waitcnt lgkmcnt(0)", "21:"]
+    set_combos(L)
     L += [
         f"s_load_dwordx16 s[{nxt}:{nxt + 15}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
         f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
@@ -658,31 +687,42 @@ def body_s8(L, j):
     if PRIO8 is not None:
         L.append("s_setprio 0")
     sfx, base = cslot_addr(j % CSLOTS8)
-    for st in range(4):
-        for q in range(4):
-            r = G(st >> 1, st & 1, 4 * q)
-            L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsc{sfx}] offset:{base + st * CS_SET + q * 1024}")
+    # per-term diagnostics of the 8-wave unit (timing only, wrong results; scripts/archive/r06_unit_breakdown.sh):
+    # s8noread no set reads, s8nodma no LDS-DMA of source rows, s8nostage no staging reads, s8noown the set writes
+    # without building the set, s8nosmem no address-stream loads (the prologue's two rows reused), s8inline a fixed
+    # coefficient's products inline per row (relative, no call)
+    if "s8noread" not in DIAG:
+        set_reads(L, sfx, base)
     L += [f"s_cmp_lg_u32 s{S_CONS}, 0", "s_cbranch_scc1 20f"]
     if "bprio" in DIAG:  # experiment: builders at raised priority while staging and building the sets
         L.append("s_setprio 1")
     nx = j + BAR8 + 1  # staged now into RB[nx % 2] (it held row nx - 2, whose set was built during row j - 1)
-    for hh in range(2):
-        r = RB(nx % 2, 4 * hh)
-        L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{(nx % SLOTS8) * 4096 + hh * 1024}")
+    if "s8nostage" not in DIAG:
+        for hh in range(2):
+            r = RB(nx % 2, 4 * hh)
+            L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsrg] offset:{(nx % SLOTS8) * 4096 + hh * 1024}")
     advance_run(L) if RUN else advance_s(L)
-    L += [f"s_add_u32 m0, s{S_LDSW}, {((j + DMA8) % SLOTS8) * 4096}", "s_nop 0",
-          "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)]  # row j + DMA8
-    own_set(L, (j + BAR8) % 2, (j + BAR8) % CSLOTS8)  # row j + BAR8's set
+    if "s8nodma" not in DIAG:
+        L += [f"s_add_u32 m0, s{S_LDSW}, {((j + DMA8) % SLOTS8) * 4096}", "s_nop 0",
+              "global_load_lds_dwordx4 %[dmaoff], s[{0}:{1}]".format(S_SRC, S_SRC + 1)]  # row j + DMA8
+    if "s8noown" in DIAG:
+        sfx2, base2 = cslot_addr((j + BAR8) % CSLOTS8)
+        L += [f"ds_write_b128 %[ldscw{sfx2}], v[{OWN(4 * q)}:{OWN(4 * q) + 3}] offset:{base2 + q * 1024}"
+              for q in range(4)]
+    else:
+        own_set(L, (j + BAR8) % 2, (j + BAR8) % CSLOTS8)  # row j + BAR8's set
     if "bprio" in DIAG:
         L.append("s_setprio 0")
-    L += ["s_waitcnt lgkmcnt(6)",  # the 16 set reads (2 staging reads + 4 set writes may fly)
+    L += [f"s_waitcnt lgkmcnt({SET_WAIT})",  # the 16 set reads (2 staging reads + 4 set writes may fly)
           "s_branch 21f", "20:", "s_waitcnt lgkmcnt(0)", "21:"]
+    set_combos(L)
     cur, nxt = S_ADDR[j % 2], S_ADDR[(j + 1) % 2]
     if RUN:  # row j is the tile's last: the next row's addresses are row 0's (the next column block, same rows)
         L += [f"s_cmp_eq_u32 s{S_CNT}, 0",
               f"s_cselect_b64 s[{S_IDX}:{S_IDX + 1}], s[{S_IDXM}:{S_IDXM + 1}], s[{S_IDX}:{S_IDX + 1}]"]
     L += [
-        f"s_load_dwordx16 s[{nxt}:{nxt + 15}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}",
+        f"s_load_dwordx16 s[{nxt}:{nxt + 15}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}" if "s8nosmem" not in DIAG
+        else "s_nop 0",
         f"s_add_u32 s{S_IDX}, s{S_IDX}, {STREAM_J_BYTES}",
         f"s_addc_u32 s{S_IDX + 1}, s{S_IDX + 1}, 0",
         f"s_set_gpr_idx_on 0, {idx_mode()}",
@@ -690,8 +730,26 @@ def body_s8(L, j):
     for i in range(NT):
         if PRIO8 is not None and i == PRIO8[0]:
             L.append(f"s_setprio {PRIO8[1]}")
+        if "s8inline" in DIAG:  # the block of a fixed coefficient inline, in the packed blocks' form
+            L.append(m0_slot(i))
+            L += inline_block(0x53 + 11 * i)
+            continue
         L += [m0_slot(i), f"s_swappc_b64 s[{S_RET}:{S_RET + 1}], s[{cur + 2 * i}:{cur + 2 * i + 1}]"]
     L.append("s_set_gpr_idx_off")
+
+
+def inline_block(c):
+    """Block c's XOR3s / XORs without its return (packed form: the accumulator is SRC0, GPR-index relative)."""
+    lo, hi = block_indices(c)
+    v3, v2 = [], []
+    for g in range(2):
+        for o in range(8):
+            a = ACC(0, g, o)
+            if lo[o] and hi[o]:
+                v3.append(f"v_bitop3_b32 v{a}, v{a}, v{G(g, 0, lo[o])}, v{G(g, 1, hi[o])} bitop3:0x96")
+            elif lo[o] or hi[o]:
+                v2.append(f"v_xor_b32 v{a}, v{a}, v{G(g, 0, lo[o]) if lo[o] else G(g, 1, hi[o])}")
+    return v3 + v2
 
 
 def program_shared8():
@@ -727,6 +785,8 @@ def program_shared8():
         L += [f"s_add_u32 m0, s{S_LDSW}, {slot * 4096}", "s_nop 0", dmai]
     L.append("22:")
     L.append(f"s_load_dwordx16 s[{S_ADDR[0]}:{S_ADDR[0] + 15}], s[{S_IDX}:{S_IDX + 1}], 0")
+    if "s8nosmem" in DIAG:  # both address buffers once, reused for every row
+        L.append(f"s_load_dwordx16 s[{S_ADDR[1]}:{S_ADDR[1] + 15}], s[{S_IDX}:{S_IDX + 1}], {STREAM_J_BYTES}")
     L += [f"v_mov_b32 v{r}, 0" for r in range(128)]
     L.append(f"v_mov_b32 v{OWN(0)}, 0")
     L += [f"s_waitcnt vmcnt({DMA8 - 1 - BAR8})", "s_barrier"]  # rows 0..BAR8 landed (consumers have no loads)
@@ -1045,6 +1105,8 @@ def main():
     # 8-wave programs keep plain stores (no gain on the VALU-bound bench, profiles/r02_cache_hint_ab.txt)
     ap.add_argument("--store-hint-small", default="nt", help="tile-store modifiers of the 1- and 2-wave programs")
     ap.add_argument("--w2split", action="store_true", help="2-wave program: waves split the byte groups, not the rows")
+    ap.add_argument("--setplanes", action="store_true",
+                    help="shared programs: exchange only the planes of each set, composites built by every wave")
     args = ap.parse_args()
     HINTS["load"], HINTS["store"] = args.load_hint, args.store_hint
     global PRIO_AT
@@ -1055,6 +1117,9 @@ def main():
     M0STEP = not args.no_m0step
     global PACK
     PACK = not args.no_pack
+    global SETPLANES, SET_WAIT
+    if args.setplanes:
+        SETPLANES, SET_WAIT = True, 3  # 2 staging reads + 1 set write in flight
     set_bar8(args.bar8)
     global PRIO8
     PRIO8 = None if args.prio8 == "off" else tuple(int(x) for x in args.prio8.split(","))

@@ -59,7 +59,9 @@ def main():
                 elif not os.environ.get("RLNC_DIAG"):
                     assert torch.equal(out, ref_enc) and torch.equal(dec, ref_dec), c
     for c in configs:
-        line = {"variant": ["perm", "nibble", "perm3", "wide2", "wide4", "bitsliced", "bitsliced-jump", "bitsliced-jump-shared"][c[0]], "tile_rows": c[1]}
+        line = {"variant": ["perm", "nibble", "perm3", "wide2", "wide4", "bitsliced", "bitsliced-jump",
+                            "bitsliced-jump-shared", "bitsliced-jump-shared-8w", "bitsliced-jump-run"][c[0]],
+                "tile_rows": c[1]}
         for name, ma in (("enc", B * n * k * L), ("dec", B * k * k * L)):
             v = sorted(res[c][name])
             line[name + "_ms_med"] = round(v[len(v) // 2], 4)
