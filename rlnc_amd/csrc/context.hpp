@@ -238,11 +238,6 @@ struct rlnc_context {
     int up_cur = 0;       // the slot being filled
     std::mutex up_mu;     // guards the ring and the upload stream
     hipStream_t up_stream = nullptr;
-    // the synchronous uploads of Encoder::new / Recoder::new: a stream of their own, so that the call streams the
-    // object API then launches its piece kernels on never carry a host-to-device copy (a launch behind a copy on its
-    // stream pays for the cross-engine dependency in the launch call itself)
-    std::mutex ob_mu;
-    hipStream_t ob_stream = nullptr;
     // device blocks of dropped encoders / recoders / decoders, reused by the next object of a similar size: a
     // hipMalloc + hipFree pair costs 0.1-0.6 ms per object, as much as a small object's whole decode
     std::mutex blk_mu;
@@ -262,10 +257,6 @@ struct rlnc_context {
                 (void)hipStreamDestroy(x);
             }
         hs_slots.clear();
-        if (ob_stream) {
-            (void)hipStreamSynchronize(ob_stream);
-            (void)hipStreamDestroy(ob_stream);
-        }
         if (up_stream) {
             (void)hipStreamSynchronize(up_stream);
             (void)hipStreamDestroy(up_stream);
@@ -351,25 +342,6 @@ struct rlnc_context {
             blk_bytes -= blk.front().first;
             blk.erase(blk.begin());
         }
-    }
-    // host -> device copy of an object's rows (dpitch / spitch / width / rows as hipMemcpy2D), synchronous, on
-    // ob_stream.  RLNC_OBJ_UPLOAD=lease (A/B knob, read once) puts it on `lease_stream` instead (the round-5 form).
-    int object_upload(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t rows,
-                      hipStream_t lease_stream) {
-        static const bool on_lease = [] {
-            const char *e = getenv("RLNC_OBJ_UPLOAD");
-            return e && std::strcmp(e, "lease") == 0;
-        }();
-        if (on_lease) {
-            HIP_TRY(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyHostToDevice, lease_stream));
-            HIP_TRY(hipStreamSynchronize(lease_stream));
-            return RLNC_OK;
-        }
-        std::lock_guard<std::mutex> lock(ob_mu);
-        if (!ob_stream) HIP_TRY(hipStreamCreateWithFlags(&ob_stream, hipStreamNonBlocking));
-        HIP_TRY(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyHostToDevice, ob_stream));
-        HIP_TRY(hipStreamSynchronize(ob_stream));
-        return RLNC_OK;
     }
     int upload_stream_locked() {
         if (!up_stream) HIP_TRY(hipStreamCreateWithFlags(&up_stream, hipStreamNonBlocking));

@@ -563,7 +563,8 @@ static int encoder_from_host(rlnc_context *ctx, const uint8_t *data, size_t len,
         if (off < len) std::memcpy(h + r * e->stride, data + off, std::min(L, len - off));
     }
     if (pad) h[(len / L) * e->stride + (len % L)] = rlnc::kBoundaryMarker;
-    if ((st = ctx->object_upload(e->src, k * e->stride, h, k * e->stride, k * e->stride, 1, ws->stream))) return st;
+    HIP_TRY(hipMemcpyAsync(e->src, h, k * e->stride, hipMemcpyHostToDevice, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
     *out = e.release();
     return RLNC_OK;
 }
@@ -723,7 +724,8 @@ int rlnc_recoder_new(rlnc_context *ctx, const uint8_t *data, size_t len, size_t 
     if ((st = ctx->obj_alloc(n * r->stride, &r->pieces, &r->pieces_cap))) return st;
     Lease ws(ctx);
     if ((st = ws.acquire())) return st;
-    if ((st = ctx->object_upload(r->pieces, r->stride, data, full, full, n, ws->stream))) return st;
+    HIP_TRY(hipMemcpy2DAsync(r->pieces, r->stride, data, full, full, n, hipMemcpyHostToDevice, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
     *out = r.release();
     return RLNC_OK;
 }

@@ -35,12 +35,16 @@ base + offset of block c (64-bit; the base is read once per device by a probe la
 it and exits), two s_load_dwordx16 buffers of 8 addresses, so a call is an M0 step (s_add_u32 m0, m0, 16) +
 s_swappc_b64 + s_setpc_b64.  Its blocks are packed (--pack): the accumulator is SRC0 (GPR-index mode SRC0 + DST),
 so a product whose low or high half selects nothing is a 4-byte v_xor_b32 instead of an XOR3 with a zero operand.
-With 4 waves on one column block, wave w builds
-only set w = (group w >> 1, half w & 1) of the plane combinations -- half of one group's transpose + 11 XORs
-instead of two full transposes + 44 XORs -- and the four sets (4 KiB each) are exchanged through two 16 KiB
-LDS slots.  Per source row j: barrier; 16 ds_read_b128 of row j's sets; the staging read of row j + 2 (the
-wave's group only); the DMA of row j + 4; the own set of row j + 1 (hides the set reads' latency); row j's
-calls.  Cost attribution (profiles/r01_bsj_diag.txt): calls ~10 %, the barrier ~7 %, the own set ~9 %.
+With 4 waves on one column block, wave w transposes
+only set w = (group w >> 1, half w & 1) of the planes -- half of one group's transpose instead of two full ones --
+and since round 6 only the four planes of each set (1 KiB) go through LDS, every wave building the 11 composite
+combinations of the four sets from them (--no-setplanes: whole 4 KiB sets, built by their builder, the round-1..5
+form); the sets are exchanged through two 16 KiB
+LDS slots.  Per source row j: barrier; 4 ds_read_b128 of row j's set planes; the staging read of row j + 2 (the
+wave's group only); the DMA of row j + 4; the own set planes of row j + 1 (hides the set reads' latency); the 44
+composite XORs of row j; row j's calls.  Cost attribution of the round-5 form (profiles/r01_bsj_diag.txt): calls
+~10 %, the barrier ~7 %, the own set ~9 %; of the 8-wave program at round 6's start
+(profiles/r06_unit_breakdown.json): set reads 11.7 %, barrier 10.1 %, calls 10.0 %, set building 5.1 %.
 Run `python3 gen_bsjump.py` after editing; the output is committed.
 """
 import argparse
@@ -65,11 +69,13 @@ def ACC(i, g, p):  # output row i, group g, plane p (the blocks name row 0; M0 a
     return i * 16 + g * 8 + p
 
 
-# --setplanes (experiment, round 6): the shared programs exchange only the 4 transposed planes of a set through LDS
-# (one ds_write_b128 per builder, one ds_read_b128 per set and wave instead of four) and every wave builds the 11
-# composite entries of each set itself (44 VOP2 XORs per source row per wave): a quarter of the LDS read traffic for
-# more VALU.  The planes sit first in each set's 16 registers (a contiguous quad), entry 0 last.
-SETPLANES = False
+# Set planes (round 6, default; --no-setplanes = the round-1..5 form): the shared programs exchange only the 4
+# transposed planes of a set through LDS (one ds_write_b128 per builder, one ds_read_b128 per set and wave instead of
+# four) and every wave builds the 11 composite entries of each set itself (44 VOP2 XORs per source row per wave): a
+# quarter of the LDS read traffic for more VALU.  The set reads were the largest term of the 8-wave unit (11.7 %,
+# profiles/r06_unit_breakdown.json); interleaved A/B (profiles/r06_setplanes_ab.txt): encode launch -2.3 %, the 4-wave
+# 32-row product -7.5 %, bench +3.3 %.  The planes sit first in each set's 16 registers (a contiguous quad), entry 0 last.
+SETPLANES = True
 SP_POS = {1: 0, 2: 1, 4: 2, 8: 3, 3: 4, 5: 5, 6: 6, 7: 7, 9: 8, 10: 9, 11: 10, 12: 11, 13: 12, 14: 13, 15: 14, 0: 15}
 
 
@@ -463,7 +469,7 @@ def set_combos(L):
             combos(st >> 1, st & 1, L)
 
 
-SET_WAIT = 6  # LDS ops a builder leaves in flight at the set-read wait: 2 staging reads + 4 set writes
+SET_WAIT = 3  # LDS ops a builder leaves in flight at the set-read wait: 2 staging reads + the set write(s) (1, or 4)
 
 
 def body_s(L, j, cons=False):
@@ -1105,8 +1111,8 @@ def main():
     # 8-wave programs keep plain stores (no gain on the VALU-bound bench, profiles/r02_cache_hint_ab.txt)
     ap.add_argument("--store-hint-small", default="nt", help="tile-store modifiers of the 1- and 2-wave programs")
     ap.add_argument("--w2split", action="store_true", help="2-wave program: waves split the byte groups, not the rows")
-    ap.add_argument("--setplanes", action="store_true",
-                    help="shared programs: exchange only the planes of each set, composites built by every wave")
+    ap.add_argument("--no-setplanes", action="store_true",
+                    help="shared programs: exchange whole sets through LDS (the round-1..5 form) instead of planes only")
     args = ap.parse_args()
     HINTS["load"], HINTS["store"] = args.load_hint, args.store_hint
     global PRIO_AT
@@ -1118,8 +1124,8 @@ def main():
     global PACK
     PACK = not args.no_pack
     global SETPLANES, SET_WAIT
-    if args.setplanes:
-        SETPLANES, SET_WAIT = True, 3  # 2 staging reads + 1 set write in flight
+    if args.no_setplanes:
+        SETPLANES, SET_WAIT = False, 6  # 2 staging reads + 4 set writes in flight
     set_bar8(args.bar8)
     global PRIO8
     PRIO8 = None if args.prio8 == "off" else tuple(int(x) for x in args.prio8.split(","))
