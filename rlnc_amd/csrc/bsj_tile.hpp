@@ -85,10 +85,12 @@ template <int W, bool SHARE, bool RUN>
 __device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stream, int row_tiles, int rt, int cb,
                                          int obj, uint32_t tiles, uint64_t *probe) {
     constexpr int kTileRows = kBsjWaveRows * W;
-    // W = 8: one workgroup per CU, so a deeper ring and 2 BAR8 set slots (the builders run BAR8 rows ahead); W = 1:
-    // a deeper ring too (its one wave alone keeps the source rows in flight)
+    // W = 8: one workgroup per CU, so a deeper ring and 2 BAR8 set slots (the builders run BAR8 rows ahead); the
+    // 4-wave shared program may take the same form (gen_bsjump.py --w4bar: RLNC_BSJ_SLOTS4S ring slots); W = 1: a
+    // deeper ring too (its one wave alone keeps the source rows in flight)
     __shared__ __attribute__((aligned(16))) uint8_t
-        ring[(W == 8 ? RLNC_BSJ_SLOTS8 : W == 1 ? RLNC_BSJ_SLOTS1 : W == 2 ? RLNC_BSJ_SLOTS2 : RLNC_BSJ_SLOTS) *
+        ring[(W == 8 ? RLNC_BSJ_SLOTS8 : W == 1 ? RLNC_BSJ_SLOTS1 : W == 2 ? RLNC_BSJ_SLOTS2
+                                                    : SHARE ? RLNC_BSJ_SLOTS4S : RLNC_BSJ_SLOTS) *
              kBsjColBlock];
     __shared__ __attribute__((aligned(16))) uint8_t cset[SHARE ? (W == 8 ? RLNC_BSJ_CSET_BYTES8 : RLNC_BSJ_CSET_BYTES) : 16];
     const int row0 = rt * kTileRows;
@@ -131,7 +133,7 @@ __device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stre
     const uint32_t dmaoff = kShare * uint32_t(ws) + 16u * lane;
     const uint32_t off = 16u * lane;
     const uint32_t ldsc = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)cset)) + 16u * lane;
-    const uint32_t ldscw = ldsc + 4096u * uint32_t(ws);      // this wave's set (group ws >> 1, half ws & 1)
+    const uint32_t ldscw = ldsc + uint32_t(RLNC_BSJ_CS_SET) * uint32_t(ws);  // this wave's set (group ws >> 1, half ws & 1)
     const uint32_t ldsrg = ldsr + 2048u * uint32_t(kSplit ? ws : ws >> 1);  // this wave's group of the ring chunk
     const uint32_t half = uint32_t(ws & 1);
     const uint32_t cons = uint32_t(w / kStageWaves);

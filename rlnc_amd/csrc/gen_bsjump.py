@@ -533,6 +533,8 @@ def program_shared(cons=False):
     saved = {n: globals()[n] for n in SHARED_SGPRS}
     globals().update(SHARED_SGPRS)
     try:
+        if not cons and W4BAR:
+            return program_shared4b()
         return program_shared_body(cons)
     finally:
         globals().update(saved)
@@ -668,14 +670,23 @@ PRIO8 = None
 
 def set_bar8(b):
     global BAR8, DMA8, SLOTS8, CSLOTS8
-    BAR8, DMA8, SLOTS8, CSLOTS8 = b, 2 * b + 2, (6 if b == 2 else 12), 2 * b
+    BAR8, DMA8, SLOTS8, CSLOTS8 = b, 2 * b + 2, {2: 6, 3: 12, 4: 16}[b], 2 * b
 
 
 set_bar8(3)
 
 
 def cslot_addr(slot):  # (base operand, offset) of set slot `slot` for reads / the wave's own write
-    return ("", slot * CS_SLOT) if slot < 4 else ("2", (slot - 4) * CS_SLOT)
+    o = slot * CS_SLOT  # ds offsets are 16-bit: slots past 64 KiB through the second base (+65536)
+    return ("", o) if o + CS_SLOT <= 65536 else ("2", o - 65536)
+
+
+def lcm(*xs):
+    import math
+    out = 1
+    for x in xs:
+        out = out * x // math.gcd(out, x)
+    return out
 
 
 def body_s8(L, j):
@@ -758,6 +769,42 @@ def inline_block(c):
     return v3 + v2
 
 
+W4BAR = 0  # --w4bar B: the 4-wave shared program in the 8-wave program's form (all four waves builders)
+
+
+def program_shared4b():
+    """The 4-wave shared program (32-row tiles: the decode's products) in the 8-wave program's form: the four waves
+    build the sets BAR8 rows ahead of their reads and meet at a barrier every BAR8-th row instead of every row (LDS:
+    SLOTS8 ring slots + CSLOTS8 set slots; with set planes 72 KiB at BAR8 = 3, two workgroups per CU).  Carries the
+    probe entry and the block table the 8-wave program calls into, like program_shared_body."""
+    assert WAVES == 4
+    L = [
+        f"s_getpc_b64 s[{S_BASE}:{S_BASE + 1}]",
+        "5:",
+        f"s_add_u32 s{S_BASE}, s{S_BASE}, (9f - 5b)",
+        f"s_addc_u32 s{S_BASE + 1}, s{S_BASE + 1}, 0",
+        # probe launch (probe != 0): store the block table's address for the offset kernel and leave
+        "s_cmp_lg_u64 %[probe], 0",
+        "s_cbranch_scc0 10f",
+        f"v_mov_b32 v{V_X}, s{S_BASE}",
+        f"v_mov_b32 v{V_X + 1}, s{S_BASE + 1}",
+        f"v_mov_b32 v{V_X + 2}, 0",
+        f"global_store_dwordx2 v{V_X + 2}, v[{V_X}:{V_X + 1}], %[probe]",
+        "s_waitcnt vmcnt(0)",
+        "s_branch 8f",
+        "10:",
+    ]
+    L += program_shared8()
+    L.append("s_branch 8f")
+    if ALIGN:
+        L.append(f".p2align {ALIGN}")
+    L.append("9:")
+    global SOFFS
+    SOFFS = blocks_packed(L)
+    L.append("8:")
+    return L
+
+
 def program_shared8():
     L = []
     if RUN:
@@ -810,7 +857,7 @@ def program_shared8():
                 L.append(f"ds_read_b128 v[{x}:{x + 3}], %[ldsrg] offset:{(r + 2) * 4096 + hh * 1024}")
         L.append("s_waitcnt lgkmcnt(0)")  # the set writes have read OWN; the staged row is in
     L += ["23:", "s_waitcnt lgkmcnt(0)"]
-    unroll = 12  # lcm of BAR8, CSLOTS8, SLOTS8 and the two RB / address buffers (12 for BAR8 = 2 and 3)
+    unroll = lcm(BAR8, CSLOTS8, SLOTS8, 2)  # set slots, ring slots and the two RB / address buffers (12 at BAR8 = 3)
     if not RUN:
         L.append("1:")
         for j in range(unroll):
@@ -1093,7 +1140,6 @@ def main():
     ap.add_argument("--diag", default="", help="comma list: novm, inline, absinline (timing diagnostics, wrong results)")
     ap.add_argument("--stride", type=int, default=DEFAULT_STRIDE, help="bytes per code block (>= 132, multiple of 4)")
     ap.add_argument("--align", type=int, default=DEFAULT_ALIGN, help="log2 alignment of the block table")
-    ap.add_argument("--bar8", type=int, default=3, choices=(2, 3), help="8-wave program: a barrier every N rows")
     ap.add_argument("--prio8", default="off", help="K,L: 8-wave program's calls K.. of each row at s_setprio L")
     ap.add_argument("--no-m0step", action="store_true", help="shared programs: M0 moved as a literal per call")
     ap.add_argument("--no-pack", action="store_true",
@@ -1111,6 +1157,9 @@ def main():
     # 8-wave programs keep plain stores (no gain on the VALU-bound bench, profiles/r02_cache_hint_ab.txt)
     ap.add_argument("--store-hint-small", default="nt", help="tile-store modifiers of the 1- and 2-wave programs")
     ap.add_argument("--w2split", action="store_true", help="2-wave program: waves split the byte groups, not the rows")
+    ap.add_argument("--w4bar", type=int, default=0, choices=(0, 2, 3),
+                    help="4-wave shared program in the 8-wave form with a barrier every N rows (0: every row)")
+    ap.add_argument("--bar8", type=int, default=3, choices=(2, 3, 4), help="8-wave program: a barrier every N rows")
     ap.add_argument("--no-setplanes", action="store_true",
                     help="shared programs: exchange whole sets through LDS (the round-1..5 form) instead of planes only")
     args = ap.parse_args()
@@ -1123,9 +1172,12 @@ def main():
     M0STEP = not args.no_m0step
     global PACK
     PACK = not args.no_pack
-    global SETPLANES, SET_WAIT
+    global SETPLANES, SET_WAIT, CS_SLOT, CS_SET, W4BAR
     if args.no_setplanes:
         SETPLANES, SET_WAIT = False, 6  # 2 staging reads + 4 set writes in flight
+    else:  # set planes: a set slot holds the four sets' planes (4 x 1 KiB)
+        CS_SLOT, CS_SET = 4096, 1024
+    W4BAR = args.w4bar
     set_bar8(args.bar8)
     global PRIO8
     PRIO8 = None if args.prio8 == "off" else tuple(int(x) for x in args.prio8.split(","))
@@ -1157,8 +1209,13 @@ def main():
             f.write(f'#define RLNC_BSJ_ASM_W{w} "{body_txt}"\n')
         WAVES, WG_ROWS = 4, NT * 4
         STREAM_J_BYTES = WG_ROWS * 8  # 64-bit block addresses
+        if W4BAR:
+            set_bar8(W4BAR)
         body_txt = "\\n\\t".join(hinted(program_shared()))
         f.write(f'#define RLNC_BSJ_ASM_W4S "{body_txt}"\n')
+        f.write(f"#define RLNC_BSJ_SLOTS4S {SLOTS8 if W4BAR else SLOTS}\n")
+        f.write(f"#define RLNC_BSJ_CSET_BYTES {(CSLOTS8 if W4BAR else 2) * CS_SLOT}\n")
+        set_bar8(args.bar8)
         WAVES, WG_ROWS = 8, NT * 8
         STREAM_J_BYTES = WG_ROWS * 8
         body_txt = "\\n\\t".join(hinted(program_shared(cons=True)))
@@ -1172,7 +1229,7 @@ def main():
         if SOFFS is not None:  # block offsets of the shared programs' packed table (bsj_offset_kernel<true>)
             f.write("#define RLNC_BSJ_SOFFSETS {" + ", ".join(str(x) for x in SOFFS) + "}\n")
         f.write(f"#define RLNC_BSJ_CSET_BYTES8 {CSLOTS8 * CS_SLOT}\n")
-        f.write(f"#define RLNC_BSJ_CSET_BYTES {2 * CS_SLOT}\n")
+        f.write(f"#define RLNC_BSJ_CS_SET {CS_SET}\n")
         f.write(f"#define RLNC_BSJ_CLOBBER_V {clob_v}\n")
         f.write(f'#define RLNC_BSJ_CLOBBER_S {clob_s}, "m0", "scc", "memory"\n')
 
