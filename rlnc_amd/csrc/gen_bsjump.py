@@ -463,8 +463,9 @@ def set_reads(L, sfx, base):
 
 
 def set_combos(L):
-    """--setplanes: the 11 composite entries of the four sets from their planes, in every wave."""
-    if SETPLANES:
+    """Set planes: the 11 composite entries of the four sets from their planes, in every wave (--diag=s8nocombo:
+    skipped, timing only)."""
+    if SETPLANES and "s8nocombo" not in DIAG:
         for st in range(4):
             combos(st >> 1, st & 1, L)
 
