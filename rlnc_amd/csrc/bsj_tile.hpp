@@ -143,8 +143,8 @@ __device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stre
     : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),                           \
       [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw), [off] "v"(off), \
       [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr), [ldsc] "v"(ldsc), [ldscw] "v"(ldscw), [ldsrg] "v"(ldsrg),           \
-      [half] "s"(half), [probe] "s"(probe), [cons] "s"(cons), [ldsc2] "v"(ldsc + 65536u),                        \
-      [ldscw2] "v"(ldscw + 65536u), [tiles] "s"(tiles)                                                            \
+      [half] "s"(half), [probe] "s"(probe), [cons] "s"(cons), [ldsc2] "v"(ldsc + uint32_t(RLNC_BSJ_CS_BASE2)),   \
+      [ldscw2] "v"(ldscw + uint32_t(RLNC_BSJ_CS_BASE2)), [tiles] "s"(tiles)                                       \
     : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S
     if constexpr (W == 1) asm volatile(RLNC_BSJ_ASM_W1 : RLNC_BSJ_OPERANDS);
     if constexpr (W == 2) asm volatile(RLNC_BSJ_ASM_W2 : RLNC_BSJ_OPERANDS);

@@ -77,10 +77,19 @@ def ACC(i, g, p):  # output row i, group g, plane p (the blocks name row 0; M0 a
 # 32-row product -7.5 %, bench +3.3 %.  The planes sit first in each set's 16 registers (a contiguous quad), entry 0 last.
 SETPLANES = True
 SP_POS = {1: 0, 2: 1, 4: 2, 8: 3, 3: 4, 5: 5, 6: 6, 7: 7, 9: 8, 10: 9, 11: 10, 12: 11, 13: 12, 14: 13, 15: 14, 0: 15}
+# --setregs R (8 or 12, A/B): R entries of each set go through LDS (the planes and the first R - 4 composites of
+# SR_ORDER, built by the set's builder), the other 15 - R composites are built by every wave; R = 4 is the planes-only
+# form above.  Each composite is one XOR of two entries earlier in SR_ORDER (SR_RECIPE).
+SETREGS = 4
+SR_ORDER = [1, 2, 4, 8, 3, 12, 5, 10, 6, 9, 7, 11, 13, 14, 15, 0]
+SR_RECIPE = {3: (1, 2), 12: (4, 8), 5: (1, 4), 10: (2, 8), 6: (2, 4), 9: (1, 8), 7: (3, 4), 11: (3, 8), 13: (5, 8),
+             14: (6, 8), 15: (7, 8)}
 
 
 def G(g, h, v):  # combination v of half h of group g (G[g][h][0] = 0)
-    return 128 + g * 32 + h * 16 + (SP_POS[v] if SETPLANES else v)
+    if not SETPLANES:
+        return 128 + g * 32 + h * 16 + v
+    return 128 + g * 32 + h * 16 + (SP_POS[v] if SETREGS == 4 else SR_ORDER.index(v))
 
 
 def RAW(g, d):  # the current source row's 64 bytes, read from the LDS ring
@@ -436,9 +445,12 @@ def own_set(L, rb, cslot):
     entries by VOP2 XORs, then 4 ds_write_b128 to set slot `cslot` (entry 0 is the zero register)."""
     L += [f"s_cmp_eq_u32 s{S_H}, 0", "s_cbranch_scc0 4f"]
     for h in range(2):
-        if SETPLANES:  # the 4 planes only, as one contiguous quad OWN(0..3)
+        if SETPLANES:  # the 4 planes as one contiguous quad OWN(0..3), then the exchanged composites OWN(4..R-1)
             planes = {4 * h + b: OWN(b) for b in range(4)}
             transpose({d: RB(rb, d) for d in range(8)}, planes, L, half=h)
+            for pos in range(4, SETREGS):
+                x, y = SR_RECIPE[SR_ORDER[pos]]
+                L.append(f"v_xor_b32 v{OWN(pos)}, v{OWN(SR_ORDER.index(x))}, v{OWN(SR_ORDER.index(y))}")
         else:
             planes = {4 * h + b: OWN(1 << b) for b in range(4)}
             transpose({d: RB(rb, d) for d in range(8)}, planes, L, half=h)
@@ -449,7 +461,7 @@ def own_set(L, rb, cslot):
         if h == 0:
             L.append("4:")
     sfx, base = cslot_addr(cslot)
-    for q in range(1 if SETPLANES else 4):
+    for q in range(SETREGS // 4 if SETPLANES else 4):
         L.append(f"ds_write_b128 %[ldscw{sfx}], v[{OWN(4 * q)}:{OWN(4 * q) + 3}] offset:{base + q * 1024}")
 
 
@@ -457,8 +469,8 @@ def set_reads(L, sfx, base):
     """The four sets of a source row from LDS: 16 ds_read_b128 (whole sets), or with --setplanes one per set (the
     planes) into the set's first quad."""
     for st in range(4):
-        for q in range(1 if SETPLANES else 4):
-            r = G(st >> 1, st & 1, 1) if SETPLANES else G(st >> 1, st & 1, 4 * q)
+        for q in range(SETREGS // 4 if SETPLANES else 4):
+            r = G(st >> 1, st & 1, 1) + 4 * q if SETPLANES else G(st >> 1, st & 1, 4 * q)
             L.append(f"ds_read_b128 v[{r}:{r + 3}], %[ldsc{sfx}] offset:{base + st * CS_SET + q * 1024}")
 
 
@@ -467,7 +479,13 @@ def set_combos(L):
     skipped, timing only)."""
     if SETPLANES and "s8nocombo" not in DIAG:
         for st in range(4):
-            combos(st >> 1, st & 1, L)
+            if SETREGS == 4:
+                combos(st >> 1, st & 1, L)
+                continue
+            g, h = st >> 1, st & 1
+            for v in SR_ORDER[SETREGS:15]:
+                x, y = SR_RECIPE[v]
+                L.append(f"v_xor_b32 v{G(g, h, v)}, v{G(g, h, x)}, v{G(g, h, y)}")
 
 
 SET_WAIT = 3  # LDS ops a builder leaves in flight at the set-read wait: 2 staging reads + the set write(s) (1, or 4)
@@ -677,9 +695,18 @@ def set_bar8(b):
 set_bar8(3)
 
 
+def cs_base2():
+    """Byte offset of the second set-slot base (%[ldsc2] / %[ldscw2]: ds offsets are 16-bit): the first slot that
+    does not end within 64 KiB of the first base (RLNC_BSJ_CS_BASE2 for the host)."""
+    first = 0
+    while (first + 1) * CS_SLOT <= 65536:
+        first += 1
+    return first * CS_SLOT
+
+
 def cslot_addr(slot):  # (base operand, offset) of set slot `slot` for reads / the wave's own write
-    o = slot * CS_SLOT  # ds offsets are 16-bit: slots past 64 KiB through the second base (+65536)
-    return ("", o) if o + CS_SLOT <= 65536 else ("2", o - 65536)
+    o, b2 = slot * CS_SLOT, cs_base2()
+    return ("", o) if o < b2 else ("2", o - b2)
 
 
 def lcm(*xs):
@@ -1161,6 +1188,8 @@ def main():
     ap.add_argument("--w4bar", type=int, default=0, choices=(0, 2, 3),
                     help="4-wave shared program in the 8-wave form with a barrier every N rows (0: every row)")
     ap.add_argument("--bar8", type=int, default=3, choices=(2, 3, 4), help="8-wave program: a barrier every N rows")
+    ap.add_argument("--setregs", type=int, default=4, choices=(4, 8, 12),
+                    help="set planes: entries of each set exchanged through LDS (4 = the planes only)")
     ap.add_argument("--no-setplanes", action="store_true",
                     help="shared programs: exchange whole sets through LDS (the round-1..5 form) instead of planes only")
     args = ap.parse_args()
@@ -1173,11 +1202,14 @@ def main():
     M0STEP = not args.no_m0step
     global PACK
     PACK = not args.no_pack
-    global SETPLANES, SET_WAIT, CS_SLOT, CS_SET, W4BAR
+    global SETPLANES, SET_WAIT, CS_SLOT, CS_SET, W4BAR, SETREGS
     if args.no_setplanes:
         SETPLANES, SET_WAIT = False, 6  # 2 staging reads + 4 set writes in flight
-    else:  # set planes: a set slot holds the four sets' planes (4 x 1 KiB)
-        CS_SLOT, CS_SET = 4096, 1024
+    else:  # set planes: a set slot holds the four sets' exchanged entries (4 x R x 256 B)
+        SETREGS = args.setregs
+        CS_SET = SETREGS * 256
+        CS_SLOT = 4 * CS_SET
+        SET_WAIT = 2 + SETREGS // 4
     W4BAR = args.w4bar
     set_bar8(args.bar8)
     global PRIO8
@@ -1231,6 +1263,7 @@ def main():
             f.write("#define RLNC_BSJ_SOFFSETS {" + ", ".join(str(x) for x in SOFFS) + "}\n")
         f.write(f"#define RLNC_BSJ_CSET_BYTES8 {CSLOTS8 * CS_SLOT}\n")
         f.write(f"#define RLNC_BSJ_CS_SET {CS_SET}\n")
+        f.write(f"#define RLNC_BSJ_CS_BASE2 {cs_base2()}\n")
         f.write(f"#define RLNC_BSJ_CLOBBER_V {clob_v}\n")
         f.write(f'#define RLNC_BSJ_CLOBBER_S {clob_s}, "m0", "scc", "memory"\n')
 

@@ -13,12 +13,14 @@ import json
 
 TERMS = {
     "s8inline": "calls: s_swappc + the block's s_setpc per (row, source), the block inlined (relative XOR3s kept)",
-    "s8noread": "set reads: 16 ds_read_b128 per wave per source row (registers left stale)",
+    "s8noread": "set reads: 16 ds_read_b128 per wave per source row (4 with set planes; registers left stale)",
     "s8noown": "set building: the builders' half transpose + 11 composite XORs (set writes kept)",
     "s8nosmem": "address stream: s_load_dwordx16 of the next row's 8 block addresses",
     "s8nobar": "barrier: s_barrier every third source row",
     "s8nodma": "LDS-DMA of source rows (global_load_lds_dwordx4)",
     "s8nostage": "staging reads of the next source row from the LDS ring",
+    "s8nocombo": "composites: the 44 VOP2 XORs per source row and wave that build the sets from their planes (set "
+                 "planes form, round 6)",
 }
 
 
