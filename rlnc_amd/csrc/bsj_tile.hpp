@@ -133,7 +133,11 @@ __device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stre
     const uint32_t dmaoff = kShare * uint32_t(ws) + 16u * lane;
     const uint32_t off = 16u * lane;
     const uint32_t ldsc = uint32_t(reinterpret_cast<uintptr_t>((lds_u8 *)cset)) + 16u * lane;
-    const uint32_t ldscw = ldsc + uint32_t(RLNC_BSJ_CS_SET) * uint32_t(ws);  // this wave's set (group ws >> 1, half ws & 1)
+    // this wave's set (group ws >> 1, half ws & 1) and the second set-slot base: per program (gen_bsjump.py --setregs4 /
+    // --setregs8, --banks)
+    constexpr uint32_t kCsSet = W == 8 ? uint32_t(RLNC_BSJ_CS_SET8) : uint32_t(RLNC_BSJ_CS_SET);
+    constexpr uint32_t kCsBase2 = W == 8 ? uint32_t(RLNC_BSJ_CS_BASE2_8) : uint32_t(RLNC_BSJ_CS_BASE2);
+    const uint32_t ldscw = ldsc + kCsSet * uint32_t(ws);
     const uint32_t ldsrg = ldsr + 2048u * uint32_t(kSplit ? ws : ws >> 1);  // this wave's group of the ring chunk
     const uint32_t half = uint32_t(ws & 1);
     const uint32_t cons = uint32_t(w / kStageWaves);
@@ -143,8 +147,8 @@ __device__ __forceinline__ void bsj_tile(const MatmulParams &p, const void *stre
     : [src] "s"(src), [idx] "s"(idx), [dst] "s"(dst), [in_row] "s"(uint32_t(p.in_row)),                           \
       [out_row] "s"(uint32_t(p.out_row)), [n_in] "s"(p.n_in), [rows] "s"(rows_w), [ldsw] "s"(ldsw), [off] "v"(off), \
       [dmaoff] "v"(dmaoff), [ldsr] "v"(ldsr), [ldsc] "v"(ldsc), [ldscw] "v"(ldscw), [ldsrg] "v"(ldsrg),           \
-      [half] "s"(half), [probe] "s"(probe), [cons] "s"(cons), [ldsc2] "v"(ldsc + uint32_t(RLNC_BSJ_CS_BASE2)),   \
-      [ldscw2] "v"(ldscw + uint32_t(RLNC_BSJ_CS_BASE2)), [tiles] "s"(tiles)                                       \
+      [half] "s"(half), [probe] "s"(probe), [cons] "s"(cons), [ldsc2] "v"(ldsc + kCsBase2),                      \
+      [ldscw2] "v"(ldscw + kCsBase2), [tiles] "s"(tiles)                                                          \
     : RLNC_BSJ_CLOBBER_V, RLNC_BSJ_CLOBBER_S
     if constexpr (W == 1) asm volatile(RLNC_BSJ_ASM_W1 : RLNC_BSJ_OPERANDS);
     if constexpr (W == 2) asm volatile(RLNC_BSJ_ASM_W2 : RLNC_BSJ_OPERANDS);

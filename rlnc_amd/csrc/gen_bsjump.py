@@ -65,7 +65,17 @@ STREAM_J_BYTES = WG_ROWS * 4  # one dword (block offset) per row of the workgrou
 
 
 # ---- register map ---------------------------------------------------------------------------------------
+# --banks (A/B, round 6): a register map in which no XOR3 of a block reads two operands from one VGPR bank (bank =
+# register mod 4): group 0's accumulators in banks 2-3 and its low / high combinations in banks 0 / 1, group 1's
+# accumulators in banks 0-1 and its combinations in banks 2 / 3.  Entry k of the four sets of a source row is then the
+# register quad 128 + 4k (set st = 2g + h in bank st), so the set exchange through LDS is laid out by entry: one
+# ds_read_b128 per entry for every wave, one ds_write_b32 per entry for its builder.
+BANKS = False
+
+
 def ACC(i, g, p):  # output row i, group g, plane p (the blocks name row 0; M0 adds 16 * i)
+    if BANKS:  # consecutive even-aligned plane pairs (the epilogue transpose's 64-bit shifts), banks 2-3 / 0-1
+        return i * 16 + 4 * (p // 2) + (p % 2) + (2 if g == 0 else 0)
     return i * 16 + g * 8 + p
 
 
@@ -86,10 +96,19 @@ SR_RECIPE = {3: (1, 2), 12: (4, 8), 5: (1, 4), 10: (2, 8), 6: (2, 4), 9: (1, 8),
              14: (6, 8), 15: (7, 8)}
 
 
-def G(g, h, v):  # combination v of half h of group g (G[g][h][0] = 0)
+def set_pos(v):  # the entry index of combination v in a set (set planes: the exchanged entries first)
     if not SETPLANES:
-        return 128 + g * 32 + h * 16 + v
-    return 128 + g * 32 + h * 16 + (SP_POS[v] if SETREGS == 4 else SR_ORDER.index(v))
+        return v
+    return SR_ORDER.index(v) if SR_MAP else SP_POS[v]
+
+
+SR_MAP = False  # the SR_ORDER register map (any program exchanging more than the planes; the blocks follow it)
+
+
+def G(g, h, v):  # combination v of half h of group g (G[g][h][0] = 0)
+    if BANKS:
+        return 128 + 4 * set_pos(v) + 2 * g + h
+    return 128 + g * 32 + h * 16 + set_pos(v)
 
 
 def RAW(g, d):  # the current source row's 64 bytes, read from the LDS ring
@@ -461,6 +480,10 @@ def own_set(L, rb, cslot):
         if h == 0:
             L.append("4:")
     sfx, base = cslot_addr(cslot)
+    if BANKS:  # entry k of this wave's set into its dword of the entry's 16 bytes (ldscw = ldsc + 4 * set)
+        for k in range(SETREGS):
+            L.append(f"ds_write_b32 %[ldscw{sfx}], v{OWN(k)} offset:{base + k * 1024}")
+        return
     for q in range(SETREGS // 4 if SETPLANES else 4):
         L.append(f"ds_write_b128 %[ldscw{sfx}], v[{OWN(4 * q)}:{OWN(4 * q) + 3}] offset:{base + q * 1024}")
 
@@ -468,6 +491,10 @@ def own_set(L, rb, cslot):
 def set_reads(L, sfx, base):
     """The four sets of a source row from LDS: 16 ds_read_b128 (whole sets), or with --setplanes one per set (the
     planes) into the set's first quad."""
+    if BANKS:  # entry k of all four sets: one quad
+        for k in range(SETREGS):
+            L.append(f"ds_read_b128 v[{128 + 4 * k}:{128 + 4 * k + 3}], %[ldsc{sfx}] offset:{base + k * 1024}")
+        return
     for st in range(4):
         for q in range(SETREGS // 4 if SETPLANES else 4):
             r = G(st >> 1, st & 1, 1) + 4 * q if SETPLANES else G(st >> 1, st & 1, 4 * q)
@@ -479,7 +506,7 @@ def set_combos(L):
     skipped, timing only)."""
     if SETPLANES and "s8nocombo" not in DIAG:
         for st in range(4):
-            if SETREGS == 4:
+            if not SR_MAP:
                 combos(st >> 1, st & 1, L)
                 continue
             g, h = st >> 1, st & 1
@@ -489,6 +516,16 @@ def set_combos(L):
 
 
 SET_WAIT = 3  # LDS ops a builder leaves in flight at the set-read wait: 2 staging reads + the set write(s) (1, or 4)
+
+
+def apply_setregs(r):
+    """The set exchange of the program about to be generated: r entries per set through LDS (set planes)."""
+    global SETREGS, CS_SET, CS_SLOT, SET_WAIT
+    SETREGS = r
+    if BANKS:  # laid out by entry: 1 KiB per entry of the four sets, a wave's set at +4 B
+        CS_SET, CS_SLOT, SET_WAIT = 4, r * 1024, 2 + r
+    else:
+        CS_SET, CS_SLOT, SET_WAIT = r * 256, r * 1024, 2 + r // 4
 
 
 def body_s(L, j, cons=False):
@@ -1190,6 +1227,10 @@ def main():
     ap.add_argument("--bar8", type=int, default=3, choices=(2, 3, 4), help="8-wave program: a barrier every N rows")
     ap.add_argument("--setregs", type=int, default=4, choices=(4, 8, 12),
                     help="set planes: entries of each set exchanged through LDS (4 = the planes only)")
+    ap.add_argument("--setregs4", type=int, default=0, choices=(0, 4, 8, 12), help="--setregs of the 4-wave program")
+    ap.add_argument("--setregs8", type=int, default=0, choices=(0, 4, 8, 12), help="--setregs of the 8-wave program")
+    ap.add_argument("--banks", action="store_true",
+                    help="set planes: the bank-conflict-free register map, sets exchanged by entry")
     ap.add_argument("--no-setplanes", action="store_true",
                     help="shared programs: exchange whole sets through LDS (the round-1..5 form) instead of planes only")
     args = ap.parse_args()
@@ -1206,10 +1247,12 @@ def main():
     if args.no_setplanes:
         SETPLANES, SET_WAIT = False, 6  # 2 staging reads + 4 set writes in flight
     else:  # set planes: a set slot holds the four sets' exchanged entries (4 x R x 256 B)
-        SETREGS = args.setregs
-        CS_SET = SETREGS * 256
-        CS_SLOT = 4 * CS_SET
-        SET_WAIT = 2 + SETREGS // 4
+        global BANKS, SR_MAP
+        BANKS = args.banks
+        R4 = args.setregs4 or args.setregs
+        R8 = args.setregs8 or args.setregs
+        SR_MAP = max(R4, R8) > 4 or BANKS
+        apply_setregs(R4)
     W4BAR = args.w4bar
     set_bar8(args.bar8)
     global PRIO8
@@ -1248,7 +1291,11 @@ def main():
         f.write(f'#define RLNC_BSJ_ASM_W4S "{body_txt}"\n')
         f.write(f"#define RLNC_BSJ_SLOTS4S {SLOTS8 if W4BAR else SLOTS}\n")
         f.write(f"#define RLNC_BSJ_CSET_BYTES {(CSLOTS8 if W4BAR else 2) * CS_SLOT}\n")
+        f.write(f"#define RLNC_BSJ_CS_SET {CS_SET}\n")
+        f.write(f"#define RLNC_BSJ_CS_BASE2 {cs_base2()}\n")
         set_bar8(args.bar8)
+        if SETPLANES:
+            apply_setregs(R8)
         WAVES, WG_ROWS = 8, NT * 8
         STREAM_J_BYTES = WG_ROWS * 8
         body_txt = "\\n\\t".join(hinted(program_shared(cons=True)))
@@ -1262,8 +1309,8 @@ def main():
         if SOFFS is not None:  # block offsets of the shared programs' packed table (bsj_offset_kernel<true>)
             f.write("#define RLNC_BSJ_SOFFSETS {" + ", ".join(str(x) for x in SOFFS) + "}\n")
         f.write(f"#define RLNC_BSJ_CSET_BYTES8 {CSLOTS8 * CS_SLOT}\n")
-        f.write(f"#define RLNC_BSJ_CS_SET {CS_SET}\n")
-        f.write(f"#define RLNC_BSJ_CS_BASE2 {cs_base2()}\n")
+        f.write(f"#define RLNC_BSJ_CS_SET8 {CS_SET}\n")
+        f.write(f"#define RLNC_BSJ_CS_BASE2_8 {cs_base2()}\n")
         f.write(f"#define RLNC_BSJ_CLOBBER_V {clob_v}\n")
         f.write(f'#define RLNC_BSJ_CLOBBER_S {clob_s}, "m0", "scc", "memory"\n')
 
