@@ -1227,8 +1227,12 @@ def main():
     ap.add_argument("--bar8", type=int, default=3, choices=(2, 3, 4), help="8-wave program: a barrier every N rows")
     ap.add_argument("--setregs", type=int, default=4, choices=(4, 8, 12),
                     help="set planes: entries of each set exchanged through LDS (4 = the planes only)")
-    ap.add_argument("--setregs4", type=int, default=0, choices=(0, 4, 8, 12), help="--setregs of the 4-wave program")
-    ap.add_argument("--setregs8", type=int, default=0, choices=(0, 4, 8, 12), help="--setregs of the 8-wave program")
+    # the shipped split (profiles/r06_banks_r48_ab.txt): the 4-wave program exchanges the planes only, the 8-wave
+    # program (four builders for eight waves) the planes and the first 4 composites
+    ap.add_argument("--setregs4", type=int, default=0, choices=(0, 4, 8, 12),
+                    help="--setregs of the 4-wave program (0: --setregs)")
+    ap.add_argument("--setregs8", type=int, default=8, choices=(0, 4, 8, 12),
+                    help="--setregs of the 8-wave program (0: --setregs)")
     ap.add_argument("--banks", action="store_true",
                     help="set planes: the bank-conflict-free register map, sets exchanged by entry")
     ap.add_argument("--no-setplanes", action="store_true",
