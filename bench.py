@@ -365,8 +365,9 @@ def parse_args(argv=None):
     ap.add_argument("--breakdown-steps", type=int, default=24,
                     help="--pipeline 2: launches of the pipeline-1 form run before the timed loop for the per-part times")
     ap.add_argument("--no-plan", action="store_true",
-                    help="A/B: the encode launch writes its own code-block address stream (the offset kernel in front of "
-                         "the product on the launch stream) instead of taking the one written ahead on the side stream")
+                    help="A/B: the encode launch and the decode's data side write their own code-block address streams "
+                         "(the offset kernel in front of each product on its stream) instead of taking the ones written "
+                         "ahead on the side stream")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay each step as one captured HIP graph (the kernels of a step, launched together)")
     args = ap.parse_args(argv)
@@ -485,6 +486,8 @@ def run_gpu(args, dist: Dist):
         return dict(pieces=torch.empty((B, n, k + L), dtype=torch.uint8, device=dev),
                     # the encode's code-block address stream, written ahead on the side stream (encode_batch_prepare)
                     plan=torch.empty(batch.encode_plan_bytes(k, B, n), dtype=torch.uint8, device=dev),
+                    # the decode's T x data address stream, written on the side stream behind the elimination
+                    dplan=torch.empty(batch.decode_apply_plan_bytes(k, m, B), dtype=torch.uint8, device=dev),
                     decoded=torch.empty((B, k, L), dtype=torch.uint8, device=dev),
                     pst=torch.empty((B, m), dtype=torch.int32, device=dev),
                     ost=torch.empty(B, dtype=torch.int32, device=dev),
@@ -535,6 +538,8 @@ def run_gpu(args, dist: Dist):
                 batch.encode_batch_headers(co, pieces, ctx_side)
                 if not args.encode_only:
                     batch.decode_batch_eliminate(received, k, T, pst, rank, ctx_side)
+                    if not args.no_plan:
+                        batch.decode_batch_apply_prepare(received, k, T, decoded, S["dplan"], ctx_side)
                 ev_elim.record()
             torch.cuda.current_stream().wait_event(ev_plan)
             if isolate:
@@ -554,8 +559,11 @@ def run_gpu(args, dist: Dist):
             if args.pipeline:
                 if not isolate:
                     torch.cuda.current_stream().wait_event(ev_elim)
-                ea.record()  # the decode's data side alone: T x data (+ its address launch and the marker scan)
-                batch.decode_batch_apply(received, k, T, rank, decoded, ost, dl, ctx)
+                ea.record()  # the decode's data side alone: T x data and the marker scan (+ the address launch: --no-plan)
+                if args.no_plan:
+                    batch.decode_batch_apply(received, k, T, rank, decoded, ost, dl, ctx)
+                else:
+                    batch.decode_batch_apply_planned(received, k, T, rank, decoded, ost, dl, S["dplan"], ctx)
                 apply_events.append((ea, e2))
             else:
                 batch.decode_batch_device(received, k, decoded, pst, ost, dl, ctx)
@@ -603,6 +611,8 @@ def run_gpu(args, dist: Dist):
                     side.wait_event(ev_done[bi])
                 batch.encode_batch_headers(co, pieces, ctx_side)
                 batch.decode_batch_eliminate(rec, k, T, pst, rank, ctx_side)
+                if not args.no_plan:
+                    batch.decode_batch_apply_prepare(rec, k, T, decoded, S["dplan"], ctx_side)
                 ev_el[bi].record()
             if i >= 2:
                 torch.cuda.current_stream().wait_event(ev_done[bi])
@@ -615,7 +625,10 @@ def run_gpu(args, dist: Dist):
             with torch.cuda.stream(s_dec):
                 s_dec.wait_event(ev_enc[bi])
                 s_dec.wait_event(ev_el[bi])
-                batch.decode_batch_apply(rec, k, T, rank, decoded, ost, dl, ctx_dec)
+                if args.no_plan:
+                    batch.decode_batch_apply(rec, k, T, rank, decoded, ost, dl, ctx_dec)
+                else:
+                    batch.decode_batch_apply_planned(rec, k, T, rank, decoded, ost, dl, S["dplan"], ctx_dec)
                 ev_done[bi].record()
             S["obj"] = (c0, c1)
 
@@ -756,8 +769,10 @@ def run_gpu(args, dist: Dist):
             "frac_live": round(dec_achieved / live, 4) if live else None,
             "traffic": dtraffic,
             "traffic_source": dtraffic_src,
-            "kernel": (f"bsj_offset_kernel + gf_matmul_bsj_kernel<4, true> + final_len_scan_kernel (decode data side: "
-                       f"{k} decoded rows from {m} received pieces x {B} objects per launch)"),
+            "kernel": (("bsj_offset_kernel + " if args.no_plan else "") +
+                       f"gf_matmul_bsj_kernel<4, true> + final_len_scan_kernel (decode data side: "
+                       f"{k} decoded rows from {m} received pieces x {B} objects per launch"
+                       + ("" if args.no_plan else "; its address stream written ahead on the side stream") + ")"),
             "kernel_ms": round(apply_ms, 4),
             "kernel_ms_how": "HIP events on the launch stream around rlnc_decode_batch_apply, in pipeline-1 launch "
                              "groups run before the timed loop (the elimination finished before the group's encode)"

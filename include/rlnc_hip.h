@@ -288,6 +288,22 @@ int rlnc_decode_batch_eliminate(rlnc_context *ctx, const uint8_t *pieces_dev, si
 int rlnc_decode_batch_apply(rlnc_context *ctx, const uint8_t *pieces_dev, size_t pieces_obj_stride, size_t k,
                             size_t L, size_t m, size_t num_objects, const uint8_t *T_dev, const int32_t *rank_dev,
                             uint8_t *decoded_dev, int32_t *object_status_dev, int64_t *data_len_dev);
+/* rlnc_decode_batch_apply with the T x data product's code-block address stream written ahead, the decode's form of
+ * rlnc_encode_batch_prepare / _data_planned: _prepare runs the (T-only) address launch on ITS context's stream into
+ * plan_dev (device memory of at least rlnc_decode_batch_apply_plan_bytes bytes) once T is final -- e.g. on the
+ * elimination's stream right behind rlnc_decode_batch_eliminate -- and _planned, with the same arguments and kernel
+ * variant, runs the product and the marker scan without it (the caller orders it after the prepare).  The plan
+ * contract is the encode plan's: prepares are remembered by the plan buffer's address with their arguments and
+ * _planned returns InvalidArgument when those differ; the caller keeps the plan buffer alive and unwritten and T
+ * unchanged from the prepare to the product.  Writes exactly what rlnc_decode_batch_apply writes. */
+size_t rlnc_decode_batch_apply_plan_bytes(size_t k, size_t m, size_t num_objects);
+int rlnc_decode_batch_apply_prepare(rlnc_context *ctx, const uint8_t *pieces_dev, size_t pieces_obj_stride, size_t k,
+                                    size_t L, size_t m, size_t num_objects, const uint8_t *T_dev, uint8_t *decoded_dev,
+                                    void *plan_dev, size_t plan_bytes);
+int rlnc_decode_batch_apply_planned(rlnc_context *ctx, const uint8_t *pieces_dev, size_t pieces_obj_stride, size_t k,
+                                    size_t L, size_t m, size_t num_objects, const uint8_t *T_dev,
+                                    const int32_t *rank_dev, uint8_t *decoded_dev, int32_t *object_status_dev,
+                                    int64_t *data_len_dev, const void *plan_dev);
 
 /* ---- wire formats on the device ------------------------------------------------------------
  * Encoder::new's padded image (encoder.rs:85-106, BOUNDARY_MARKER consts.rs:5) built by a kernel from a byte

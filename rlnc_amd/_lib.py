@@ -118,6 +118,11 @@ _SIGS = {
                                               vp, vp, vp]),
     "rlnc_decode_batch_apply": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp,
                                           vp, vp, vp, vp]),
+    "rlnc_decode_batch_apply_plan_bytes": (C.c_size_t, [C.c_size_t, C.c_size_t, C.c_size_t]),
+    "rlnc_decode_batch_apply_prepare": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
+                                                  vp, vp, vp, C.c_size_t]),
+    "rlnc_decode_batch_apply_planned": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t,
+                                                  vp, vp, vp, vp, vp, vp]),
     "rlnc_recode_batch": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp, C.c_size_t, vp]),
     "rlnc_decode_batch": (C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t, vp, i32p,
                                     i32p, u64p]),

@@ -207,6 +207,47 @@ def decode_batch_apply(pieces, k: int, T, rank, decoded, object_status, data_len
                                           C.c_void_p(data_len.data_ptr())), ctx.lib)
 
 
+def decode_apply_plan_bytes(k: int, m: int, nobj: int) -> int:
+    """Device bytes of a decode plan buffer (decode_batch_apply_prepare)."""
+    from ._lib import load
+
+    return int(load().rlnc_decode_batch_apply_plan_bytes(k, m, nobj))
+
+
+def decode_batch_apply_prepare(pieces, k: int, T, decoded, plan, ctx: Context | None = None):
+    """The code-block address stream of decode_batch_apply(pieces, k, T, ..., decoded) written ahead into `plan` (a
+    uint8 device tensor of decode_apply_plan_bytes bytes) on this context's stream, once T is final -- e.g. behind
+    decode_batch_eliminate on its side stream, so that the data side does not wait for it
+    (decode_batch_apply_planned)."""
+    nobj, m, L, obj_stride = _pieces_view(pieces, k)
+    _chk(T, (nobj, k, m))
+    _chk(decoded, (nobj, k, L))
+    _chk(plan)
+    ctx = _ctx_for(pieces, ctx)
+    check(ctx.lib.rlnc_decode_batch_apply_prepare(ctx.h, C.c_void_p(pieces.data_ptr()), obj_stride, k, L, m, nobj,
+                                                  C.c_void_p(T.data_ptr()), C.c_void_p(decoded.data_ptr()),
+                                                  C.c_void_p(plan.data_ptr()), plan.numel()), ctx.lib)
+
+
+def decode_batch_apply_planned(pieces, k: int, T, rank, decoded, object_status, data_len, plan,
+                               ctx: Context | None = None):
+    """decode_batch_apply with the address stream prepared by decode_batch_apply_prepare (same arguments); the caller
+    orders this launch after the prepare."""
+    import torch
+
+    nobj, m, L, obj_stride = _pieces_view(pieces, k)
+    _chk(T, (nobj, k, m))
+    _chk(decoded, (nobj, k, L))
+    assert object_status.dtype == torch.int32 and data_len.dtype == torch.int64
+    ctx = _ctx_for(pieces, ctx)
+    check(ctx.lib.rlnc_decode_batch_apply_planned(ctx.h, C.c_void_p(pieces.data_ptr()), obj_stride, k, L, m, nobj,
+                                                  C.c_void_p(T.data_ptr()), C.c_void_p(rank.data_ptr()),
+                                                  C.c_void_p(decoded.data_ptr()),
+                                                  C.c_void_p(object_status.data_ptr()),
+                                                  C.c_void_p(data_len.data_ptr()), C.c_void_p(plan.data_ptr())),
+          ctx.lib)
+
+
 def matmul(coef, inp, out, ctx: Context | None = None) -> None:
     """out[o] = coef[o] ⊗ inp[o] over GF(2^8); coef [obj][n_out][n_in], inp [obj][n_in][W], out [obj][n_out][W]."""
     nobj, n_out, n_in = coef.shape

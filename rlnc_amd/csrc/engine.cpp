@@ -1188,6 +1188,8 @@ static rlnc::MatmulParams encode_batch_params(const uint8_t *src, size_t k, size
 
 // Block-address streams written ahead by rlnc_encode_batch_prepare (any context, any stream), by buffer: the product
 // they were written for and their layout.  rlnc_encode_batch_data_planned uses one only for exactly that product.
+// The decode's data side has the same pair (rlnc_decode_batch_apply_prepare / _planned): kind 1, with src = the
+// received pieces, coeffs = T, pieces = the decoded output, n = m and the pieces' object stride.
 struct EncodePlanRec {
     int device;
     const uint8_t *src, *coeffs;
@@ -1195,10 +1197,33 @@ struct EncodePlanRec {
     size_t k, L, nobj, n;
     int variant;
     rlnc::BsjStreamPlan plan;
+    int kind = 0;  // 0 encode, 1 decode apply
+    size_t obj_stride = 0;
 };
 static std::mutex g_plan_mu;
 static std::vector<std::pair<const void *, EncodePlanRec>> g_plans;  // (buffer, record), most recent last
 constexpr size_t kPlanRecs = 64;
+
+static void remember_plan(const void *buf, const EncodePlanRec &rec) {
+    std::lock_guard<std::mutex> lock(g_plan_mu);
+    for (auto it = g_plans.begin(); it != g_plans.end(); ++it)
+        if (it->first == buf) {
+            g_plans.erase(it);
+            break;
+        }
+    if (g_plans.size() >= kPlanRecs) g_plans.erase(g_plans.begin());
+    g_plans.emplace_back(buf, rec);
+}
+
+static bool find_plan(const void *buf, EncodePlanRec *rec) {
+    std::lock_guard<std::mutex> lock(g_plan_mu);
+    for (auto it = g_plans.rbegin(); it != g_plans.rend(); ++it)
+        if (it->first == buf) {
+            *rec = it->second;
+            return true;
+        }
+    return false;
+}
 
 static int encode_batch_impl(rlnc_context *ctx, const uint8_t *src, size_t k, size_t L, size_t nobj,
                              const uint8_t *coeffs, size_t n, uint8_t *pieces, bool headers,
@@ -1213,17 +1238,9 @@ static int encode_batch_impl(rlnc_context *ctx, const uint8_t *src, size_t k, si
     rlnc::MatmulParams p = encode_batch_params(src, k, L, nobj, coeffs, n, pieces, headers);
     if (plan_buf) {
         EncodePlanRec rec{};
-        bool found = false;
-        {
-            std::lock_guard<std::mutex> lock(g_plan_mu);
-            for (auto it = g_plans.rbegin(); it != g_plans.rend(); ++it)
-                if (it->first == plan_buf) {
-                    rec = it->second;
-                    found = true;
-                    break;
-                }
-        }
-        if (!found || rec.device != ctx->device || rec.src != src || rec.coeffs != coeffs || rec.pieces != pieces ||
+        const bool found = find_plan(plan_buf, &rec);
+        if (!found || rec.kind != 0 || rec.device != ctx->device || rec.src != src || rec.coeffs != coeffs ||
+            rec.pieces != pieces ||
             rec.k != k || rec.L != L || rec.nobj != nobj || rec.n != n || rec.variant != int(ctx->variant))
             return set_error(RLNC_ERR_INVALID_ARGUMENT,
                              "encode plan %p was not prepared for this product (same buffers, shape, device and kernel "
@@ -1269,14 +1286,7 @@ int rlnc_encode_batch_prepare(rlnc_context *ctx, const uint8_t *src, size_t k, s
     if (!(ctx->max_tile_rows > 0 && p.n_out > ctx->max_tile_rows))
         HIP_TRY(rlnc::launch_bsj_stream(p, ctx->variant, ctx->stream, plan_buf, plan_bytes, plan));
     EncodePlanRec rec{ctx->device, src, coeffs, pieces, k, L, nobj, n, int(ctx->variant), plan};
-    std::lock_guard<std::mutex> lock(g_plan_mu);
-    for (auto it = g_plans.begin(); it != g_plans.end(); ++it)
-        if (it->first == plan_buf) {
-            g_plans.erase(it);
-            break;
-        }
-    if (g_plans.size() >= kPlanRecs) g_plans.erase(g_plans.begin());
-    g_plans.emplace_back(plan_buf, rec);
+    remember_plan(plan_buf, rec);
     return RLNC_OK;
 }
 
@@ -1383,17 +1393,13 @@ static bool fused_scan_enabled() {
     return on;
 }
 
-// The data side: decoded = T × received data (one matmul), then the marker scan (decoder.rs:136-177).
-static int decode_apply_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
-                             size_t m, size_t nobj, const uint8_t *T, const int32_t *rank_dev, uint8_t *decoded,
-                             int32_t *ostat_dev, int64_t *len_dev, const void *bsj = nullptr, int bsj_rows = 0,
-                             const int32_t *need_dev = nullptr) {
-    const size_t full = k + L;
-    int st;
+// The data side's product: decoded = T × the received pieces' data
+static rlnc::MatmulParams decode_apply_params(const uint8_t *pieces, size_t obj_stride, size_t k, size_t L, size_t m,
+                                              size_t nobj, const uint8_t *T, uint8_t *decoded) {
     rlnc::MatmulParams p{};
     p.in = pieces + k;
     p.in_obj = int64_t(obj_stride);
-    p.in_row = int64_t(full);
+    p.in_row = int64_t(k + L);
     p.coef = T;
     p.coef_obj = int64_t(k * m);
     p.coef_row = int64_t(m);
@@ -1404,8 +1410,19 @@ static int decode_apply_impl(rlnc_context *ctx, const uint8_t *pieces, size_t ob
     p.n_in = int(m);
     p.width = int64_t(L);
     p.n_obj = int(nobj);
+    return p;
+}
+
+// The data side: decoded = T × received data (one matmul), then the marker scan (decoder.rs:136-177).
+static int decode_apply_impl(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
+                             size_t m, size_t nobj, const uint8_t *T, const int32_t *rank_dev, uint8_t *decoded,
+                             int32_t *ostat_dev, int64_t *len_dev, const void *bsj = nullptr, int bsj_rows = 0,
+                             const int32_t *need_dev = nullptr, bool bsj_abs = false) {
+    int st;
+    rlnc::MatmulParams p = decode_apply_params(pieces, obj_stride, k, L, m, nobj, T, decoded);
     p.bsj_stream = bsj;
     p.bsj_stream_rows = bsj_rows;
+    p.bsj_stream_abs = bsj_abs;
     // need_dev: the elimination already wrote every object's status and length from its payload tail; the objects
     // whose tail was all zero are scanned by their product workgroup when each object is one tile (configs[0]'s shape),
     // else the scan kernel runs over all of them
@@ -1630,6 +1647,50 @@ int rlnc_decode_batch_apply(rlnc_context *ctx, const uint8_t *pieces, size_t obj
     CHECK_ARG(T_dev && rank_dev && object_status_dev && data_len_dev);
     return decode_apply_impl(ctx, pieces, obj_stride, k, L, m, nobj, T_dev, rank_dev, decoded, object_status_dev,
                              data_len_dev);
+}
+
+size_t rlnc_decode_batch_apply_plan_bytes(size_t k, size_t m, size_t nobj) {
+    if (k == 0 || m == 0 || nobj == 0 || k > 0x7FFFFFFF || m > 0x7FFFFFFF || nobj > 0x7FFFFFFF) return 0;
+    return rlnc::bsj_stream_bytes_bound(int(nobj), int(k), int(m));
+}
+
+int rlnc_decode_batch_apply_prepare(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
+                                    size_t m, size_t nobj, const uint8_t *T_dev, uint8_t *decoded, void *plan_buf,
+                                    size_t plan_bytes) {
+    if (nobj == 0 && ctx) return RLNC_OK;
+    int st = decode_batch_check(ctx, pieces, obj_stride, k, L, m, nobj, decoded);
+    if (st) return st;
+    CHECK_ARG(T_dev && plan_buf && plan_bytes >= rlnc_decode_batch_apply_plan_bytes(k, m, nobj));
+    const rlnc::MatmulParams p = decode_apply_params(pieces, obj_stride, k, L, m, nobj, T_dev, decoded);
+    rlnc::BsjStreamPlan plan;
+    if (!(ctx->max_tile_rows > 0 && p.n_out > ctx->max_tile_rows))
+        HIP_TRY(rlnc::launch_bsj_stream(p, ctx->variant, ctx->stream, plan_buf, plan_bytes, plan));
+    EncodePlanRec rec{ctx->device, pieces, T_dev, decoded, k, L, nobj, m, int(ctx->variant), plan};
+    rec.kind = 1;
+    rec.obj_stride = obj_stride;
+    remember_plan(plan_buf, rec);
+    return RLNC_OK;
+}
+
+int rlnc_decode_batch_apply_planned(rlnc_context *ctx, const uint8_t *pieces, size_t obj_stride, size_t k, size_t L,
+                                    size_t m, size_t nobj, const uint8_t *T_dev, const int32_t *rank_dev,
+                                    uint8_t *decoded, int32_t *object_status_dev, int64_t *data_len_dev,
+                                    const void *plan_buf) {
+    if (nobj == 0 && ctx) return RLNC_OK;
+    int st = decode_batch_check(ctx, pieces, obj_stride, k, L, m, nobj, decoded);
+    if (st) return st;
+    CHECK_ARG(T_dev && rank_dev && object_status_dev && data_len_dev && plan_buf);
+    EncodePlanRec rec{};
+    if (!find_plan(plan_buf, &rec) || rec.kind != 1 || rec.device != ctx->device || rec.src != pieces ||
+        rec.coeffs != T_dev || rec.pieces != decoded || rec.obj_stride != obj_stride || rec.k != k || rec.L != L ||
+        rec.nobj != nobj || rec.n != m || rec.variant != int(ctx->variant))
+        return set_error(RLNC_ERR_INVALID_ARGUMENT,
+                         "decode plan %p was not prepared for this product (same buffers, shape, device and kernel "
+                         "variant): call rlnc_decode_batch_apply_prepare with the arguments of this call",
+                         plan_buf);
+    return decode_apply_impl(ctx, pieces, obj_stride, k, L, m, nobj, T_dev, rank_dev, decoded, object_status_dev,
+                             data_len_dev, rec.plan.tile_rows > 0 ? plan_buf : nullptr, rec.plan.tile_rows, nullptr,
+                             rec.plan.abs);
 }
 
 // ------------------------------------------------------------------------------------------------------

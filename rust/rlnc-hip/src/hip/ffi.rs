@@ -380,6 +380,35 @@ unsafe extern "C" {
         object_status_dev: *mut i32,
         data_len_dev: *mut i64,
     ) -> c_int;
+    pub fn rlnc_decode_batch_apply_plan_bytes(k: usize, m: usize, num_objects: usize) -> usize;
+    pub fn rlnc_decode_batch_apply_prepare(
+        ctx: *mut rlnc_context,
+        pieces_dev: *const u8,
+        pieces_obj_stride: usize,
+        k: usize,
+        L: usize,
+        m: usize,
+        num_objects: usize,
+        T_dev: *const u8,
+        decoded_dev: *mut u8,
+        plan_dev: *mut c_void,
+        plan_bytes: usize,
+    ) -> c_int;
+    pub fn rlnc_decode_batch_apply_planned(
+        ctx: *mut rlnc_context,
+        pieces_dev: *const u8,
+        pieces_obj_stride: usize,
+        k: usize,
+        L: usize,
+        m: usize,
+        num_objects: usize,
+        T_dev: *const u8,
+        rank_dev: *const i32,
+        decoded_dev: *mut u8,
+        object_status_dev: *mut i32,
+        data_len_dev: *mut i64,
+        plan_dev: *const c_void,
+    ) -> c_int;
 
     // wire formats on the device
     pub fn rlnc_padded_piece_byte_len(data_len: usize, k: usize) -> usize;

@@ -49,8 +49,10 @@ def main():
         # product on its stream and the marker scan right after it (first launch of each name after the product)
         picked = launches[a.skip:a.skip + a.steps]
         by_name = {}
+        # the address launch counts only where it runs inside the window (bench.py --no-plan)
+        names = ("bsj_offset_kernel", "final_len") if "bsj_offset_kernel" in line[key]["kernel"] else ("final_len",)
         for st0, d in picked:
-            for name in ("bsj_offset_kernel", "final_len"):
+            for name in names:
                 cand = [(st, dur / 1e3) for nm, gx, wx, st, dur in rows if name in nm and
                         (st < st0 if name == "bsj_offset_kernel" else st > st0)]
                 if cand:

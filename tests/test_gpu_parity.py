@@ -927,6 +927,76 @@ def test_encode_plan_written_ahead(orc, variant, k, L, n):
 
 
 
+@pytest.mark.parametrize("variant", [8, 7])
+@pytest.mark.parametrize("k,L,m", [(32, 4096 * 2, 32), (40, 4096 * 3 + 17, 44), (16, 8192, 16), (16, 4096, 20),
+                                   (8, 3000, 8)])
+def test_decode_apply_plan_written_ahead(orc, variant, k, L, m):
+    """rlnc_decode_batch_apply_prepare on the elimination's context / stream writes the T x data product's address
+    stream once T is final; rlnc_decode_batch_apply_planned (ordered after it by an event) writes exactly what
+    decode_batch_apply writes -- decoded rows, object statuses and lengths -- and full-rank objects decode to the
+    oracle's padded source with its data length (decoder.rs:136-177).  Shapes: 32-row products (the 4-wave program),
+    40 rows (the 8-wave program, misaligned rows), small objects (1- / 2-wave programs), a narrow shape (no stream);
+    one object with a rank-deficient draw.  A plan is refused for any other product (another output buffer) and an
+    encode plan is refused by the decode."""
+    import torch
+
+    import rlnc_amd
+    from rlnc_amd import batch
+    from rlnc_amd.errors import RLNCError
+
+    rng = np.random.default_rng(k * 7 + m + variant)
+    nobj = 3
+    lens = [k * L - 1 - o for o in range(nobj)]
+    srcs = [orc.pad(rng.integers(0, 256, n, dtype=np.uint8), k) for n in lens]
+    pieces_h = np.zeros((nobj, m, k + L), np.uint8)
+    for o in range(nobj):
+        co = rng.integers(0, 256, (m, k), dtype=np.uint8)
+        if o == 2:
+            co[:, 0] = 0  # rank-deficient: column 0 never pivots
+        pieces_h[o] = orc.encode(srcs[o], co)
+    pieces = dev(pieces_h)
+    c1, c2 = rlnc_amd.Context(0), rlnc_amd.Context(0)
+    for c in (c1, c2):
+        c.set_kernel_variant(variant)
+
+    def z(shape, dtype):
+        return torch.zeros(shape, dtype=dtype, device="cuda:0")
+
+    T, pst, rank = z((nobj, k, m), torch.uint8), z((nobj, m), torch.int32), z(nobj, torch.int32)
+    outs = [(z((nobj, k, L), torch.uint8), z(nobj, torch.int32), z(nobj, torch.int64)) for _ in range(2)]
+    plan = z(batch.decode_apply_plan_bytes(k, m, nobj), torch.uint8)
+    side = torch.cuda.Stream()
+    ev = torch.cuda.Event()
+    with torch.cuda.stream(side):
+        batch.decode_batch_eliminate(pieces, k, T, pst, rank, c2)
+        batch.decode_batch_apply_prepare(pieces, k, T, outs[0][0], plan, c2)
+        ev.record()
+    torch.cuda.current_stream().wait_event(ev)
+    batch.decode_batch_apply_planned(pieces, k, T, rank, *outs[0], plan, c1)
+    batch.decode_batch_apply(pieces, k, T, rank, *outs[1], c1)
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    dec, ost, dl = (host(t) for t in outs[0])
+    rk = host(rank)
+    for o in range(nobj):
+        if rk[o] == k:
+            assert np.array_equal(dec[o], srcs[o]), o
+            assert ost[o] == 0 and dl[o] == lens[o], (o, ost[o], dl[o])
+        else:
+            assert o == 2 and ost[o] == 10, (o, rk[o], ost[o])  # NotAllPiecesReceivedYet
+    with pytest.raises(RLNCError):  # another output buffer: not the product the plan was prepared for
+        batch.decode_batch_apply_planned(pieces, k, T, rank, *outs[1], plan, c1)
+    eplan = z(batch.encode_plan_bytes(k, nobj, m), torch.uint8)
+    src_d = z((nobj, k, L), torch.uint8)
+    batch.encode_batch_prepare(src_d, z((nobj, m, k), torch.uint8), z((nobj, m, k + L), torch.uint8), eplan, c1)
+    with pytest.raises(RLNCError):  # an encode plan
+        batch.decode_batch_apply_planned(pieces, k, T, rank, *outs[0], eplan, c1)
+    torch.cuda.synchronize()
+    c1.close()
+    c2.close()
+
+
 @pytest.mark.parametrize("k", [16, 8, 5])
 def test_decode_small_objects_marker_outcomes(ctx, k):
     """Objects of k <= 16 pieces x one 4 KiB column block (the small-object elimination + 1- / 2-wave product, then
