@@ -719,9 +719,10 @@ def run_init(L):
 # SLOTS8 = 12 (144 KiB; set slots 4-5 through the second base, ds offsets are 16-bit).
 BAR8 = 3
 DMA8 = SLOTS8 = CSLOTS8 = 0
-# no wave priority in the 8-wave program (its consumer waves have no set building to overtake): -0.8 % encode
-# time against calls 2.. at level 2 (profiles/r01_launch_size.txt)
-PRIO8 = None
+# 8-wave program: calls 4.. of each row at s_setprio 1, back to 0 at the next row's top (round 6 with set planes:
+# encode launch -0.9 %, bench +0.7 % interleaved, profiles/r06_prio_ab.txt; round 1's program measured no priority
+# best, -0.8 % against calls 2.. at level 2, profiles/r01_launch_size.txt)
+PRIO8 = (4, 1)
 
 
 def set_bar8(b):
@@ -1205,7 +1206,7 @@ def main():
     ap.add_argument("--diag", default="", help="comma list: novm, inline, absinline (timing diagnostics, wrong results)")
     ap.add_argument("--stride", type=int, default=DEFAULT_STRIDE, help="bytes per code block (>= 132, multiple of 4)")
     ap.add_argument("--align", type=int, default=DEFAULT_ALIGN, help="log2 alignment of the block table")
-    ap.add_argument("--prio8", default="off", help="K,L: 8-wave program's calls K.. of each row at s_setprio L")
+    ap.add_argument("--prio8", default="4,1", help="K,L: 8-wave program's calls K.. of each row at s_setprio L (off)")
     ap.add_argument("--no-m0step", action="store_true", help="shared programs: M0 moved as a literal per call")
     ap.add_argument("--no-pack", action="store_true",
                     help="shared programs: fixed-stride XOR3-only blocks (A/B history: bsj_tile.hpp requires packed)")
