@@ -222,10 +222,23 @@ def transpose(src, dst, lines, half=None):
     stage(0, mid, dst, lines, need)
 
 
+# --combo3 (A/B, round 6): the composite combinations as VOP3 v_bitop3_b32 (S0 ^ S1, S2 = 0) instead of VOP2 v_xor_b32:
+# at 2 waves per SIMD the VOP2 XOR measured 2.97 cycles per wave64 instruction against 2.38 for v_bitop3
+# (profiles/r01_ubench_ops.jsonl; equal at 4 waves per SIMD)
+COMBO3 = False
+
+
+def xor2(d, a, b):
+    """d = a ^ b for the composite combinations (register names as strings)."""
+    if COMBO3:
+        return f"v_bitop3_b32 {d}, {a}, {b}, 0 bitop3:0x3c"
+    return f"v_xor_b32 {d}, {a}, {b}"
+
+
 def combos(g, h, lines):
     """G[v] for the 11 composite v from the 4 planes (entries 1, 2, 4, 8): one VOP2 XOR each."""
     b = lambda x: v(G(g, h, x))
-    lines += [f"v_xor_b32 {b(x)}, {b(y)}, {b(z)}" for x, y, z in
+    lines += [xor2(b(x), b(y), b(z)) for x, y, z in
               [(3, 1, 2), (5, 1, 4), (6, 2, 4), (7, 3, 4), (9, 1, 8), (10, 2, 8), (11, 3, 8), (12, 4, 8), (13, 5, 8),
                (14, 6, 8), (15, 7, 8)]]
 
@@ -469,7 +482,7 @@ def own_set(L, rb, cslot):
             transpose({d: RB(rb, d) for d in range(8)}, planes, L, half=h)
             for pos in range(4, SETREGS):
                 x, y = SR_RECIPE[SR_ORDER[pos]]
-                L.append(f"v_xor_b32 v{OWN(pos)}, v{OWN(SR_ORDER.index(x))}, v{OWN(SR_ORDER.index(y))}")
+                L.append(xor2(f"v{OWN(pos)}", f"v{OWN(SR_ORDER.index(x))}", f"v{OWN(SR_ORDER.index(y))}"))
         else:
             planes = {4 * h + b: OWN(1 << b) for b in range(4)}
             transpose({d: RB(rb, d) for d in range(8)}, planes, L, half=h)
@@ -512,7 +525,7 @@ def set_combos(L):
             g, h = st >> 1, st & 1
             for v in SR_ORDER[SETREGS:15]:
                 x, y = SR_RECIPE[v]
-                L.append(f"v_xor_b32 v{G(g, h, v)}, v{G(g, h, x)}, v{G(g, h, y)}")
+                L.append(xor2(f"v{G(g, h, v)}", f"v{G(g, h, x)}", f"v{G(g, h, y)}"))
 
 
 SET_WAIT = 3  # LDS ops a builder leaves in flight at the set-read wait: 2 staging reads + the set write(s) (1, or 4)
@@ -1234,6 +1247,7 @@ def main():
                     help="--setregs of the 4-wave program (0: --setregs)")
     ap.add_argument("--setregs8", type=int, default=8, choices=(0, 4, 8, 12),
                     help="--setregs of the 8-wave program (0: --setregs)")
+    ap.add_argument("--combo3", action="store_true", help="composite combinations as v_bitop3_b32 (A/B)")
     ap.add_argument("--banks", action="store_true",
                     help="set planes: the bank-conflict-free register map, sets exchanged by entry")
     ap.add_argument("--no-setplanes", action="store_true",
@@ -1248,6 +1262,8 @@ def main():
     M0STEP = not args.no_m0step
     global PACK
     PACK = not args.no_pack
+    global COMBO3
+    COMBO3 = args.combo3
     global SETPLANES, SET_WAIT, CS_SLOT, CS_SET, W4BAR, SETREGS
     if args.no_setplanes:
         SETPLANES, SET_WAIT = False, 6  # 2 staging reads + 4 set writes in flight
