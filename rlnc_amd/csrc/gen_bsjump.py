@@ -1247,7 +1247,8 @@ def main():
                     help="--setregs of the 4-wave program (0: --setregs)")
     ap.add_argument("--setregs8", type=int, default=8, choices=(0, 4, 8, 12),
                     help="--setregs of the 8-wave program (0: --setregs)")
-    ap.add_argument("--combo3", action="store_true", help="composite combinations as v_bitop3_b32 (A/B)")
+    ap.add_argument("--combo3", action="store_true", help="composite combinations as v_bitop3_b32 in every program (A/B)")
+    ap.add_argument("--combo3-8", action="store_true", help="... in the 8-wave programs only")
     ap.add_argument("--banks", action="store_true",
                     help="set planes: the bank-conflict-free register map, sets exchanged by entry")
     ap.add_argument("--no-setplanes", action="store_true",
@@ -1317,6 +1318,8 @@ def main():
         set_bar8(args.bar8)
         if SETPLANES:
             apply_setregs(R8)
+        if args.combo3_8:
+            COMBO3 = True
         WAVES, WG_ROWS = 8, NT * 8
         STREAM_J_BYTES = WG_ROWS * 8
         body_txt = "\\n\\t".join(hinted(program_shared(cons=True)))
