@@ -369,7 +369,8 @@ def parse_args(argv=None):
                          "(the offset kernel in front of each product on its stream) instead of taking the ones written "
                          "ahead on the side stream")
     ap.add_argument("--graph", type=int, default=0,
-                    help="1: replay each step as one captured HIP graph (the kernels of a step, launched together)")
+                    help="1: replay each step as one captured HIP graph (the kernels of a step, launched together; "
+                         "the launch groups take the --pipeline 1 form: --pipeline 2 overlaps eager launches only)")
     args = ap.parse_args(argv)
     if args.workload in WORKLOADS:
         w = WORKLOADS[args.workload]
@@ -580,7 +581,7 @@ def run_gpu(args, dist: Dist):
     # (launch stream) and decode data side (decode stream) wait only for group i-2's decode to release that
     # set, so group i+1's encode fills the GPU beside group i's decode (no tail or launch gaps between the big
     # kernels).  Every group still does all of its work.
-    pipelined = args.pipeline == 2 and not args.encode_only
+    pipelined = args.pipeline == 2 and not args.encode_only and not args.graph  # a graph replays the serial step
     if pipelined:
         sets.append(buffers(C))
         ctx_dec = rlnc_amd.Context(device)
@@ -641,13 +642,17 @@ def run_gpu(args, dist: Dist):
     if args.graph:
         # eager warmup steps (they also give the per-kernel breakdown), then capture one step's launches into
         # a graph: the timed steps replay it, identical kernels and work, without per-launch host overhead
-        for _ in range(max(args.warmup, 2)):
+        eager = max(args.warmup, 2)
+        for _ in range(eager):
             step_serial()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             step_serial()
         run = g.replay
+        for evs in (enc_events, dec_events, apply_events, plan_events):
+            del evs[eager * len(chunks):]  # events recorded under capture are graph nodes, not timestamps
+        skip = len(chunks)  # the per-part times: the eager steps after the first
     elif pipelined:
         # the per-part times (encode launch for the roofline, decode) come from pipeline-1 launch groups run
         # before the timed loop (the first 6 discarded: clocks and caches settle): a kernel's own duration, not
@@ -733,11 +738,12 @@ def run_gpu(args, dist: Dist):
         "kernel_ms": round(enc_ms, 4),
         # the code-block address launch (rlnc_encode_batch_prepare) on the side stream, outside kernel_ms
         "address_stream_ms": round(plan_ms, 4) if plan_ms is not None else None,
-        "kernel_ms_how": ("HIP events around the encode launch on its stream, in pipeline-1 launch groups run "
+        "kernel_ms_how": (("HIP events around the encode launch on its stream, in pipeline-1 launch groups run "
                           "before the timed loop, the elimination finished before it (the kernel alone)")
                          if pipelined else
                          ("HIP events around the encode launch on its stream (the elimination beside it)")
-                         if args.pipeline else "HIP events around the encode launch",
+                         if args.pipeline else "HIP events around the encode launch")
+                        + (" (--graph 1: in the eager steps before the capture)" if args.graph else ""),
         "multiply_adds_per_launch": ma_per_launch,
         "ceiling": ceiling,
         "hbm": {"compulsory_bytes": enc_compulsory,
@@ -858,7 +864,8 @@ def run_gpu(args, dist: Dist):
                                      "written ahead on the side stream (rlnc_encode_batch_prepare)",
             "pipeline": {0: "serial", 1: "elimination on a side stream concurrent with the encode data work",
                          2: "elimination beside the encode data work, and launch group i+1's encode beside group "
-                            "i's decode (two buffer sets)"}[args.pipeline],
+                            "i's decode (two buffer sets)"}[1 if args.pipeline == 2 and not pipelined else args.pipeline]
+                        + (", replayed as one captured HIP graph per step" if args.graph else ""),
         },
         "roofline": roofline,
         "roofline_decode": roofline_decode,
