@@ -230,6 +230,25 @@ int piece_chunk_blocks() {
     return c;
 }
 
+bool piece_chunk_forced() {
+    static const bool f = getenv("RLNC_PIECE_CHUNK") != nullptr;
+    return f;
+}
+
+// Waves of a column-split workgroup (piece.hpp col_waves: each wave owns 1 KiB of columns and walks every source), or
+// 0 for the source-split form.  RLNC_PIECE_COLW (A/B knob, read once): W = column-split with W waves for every call
+// that does not split its sources over workgroups, 0 / unset = the source-split form
+int piece_col_waves_for(int n_in, int64_t blocks) {
+    static const int forced = [] {
+        const char *e = getenv("RLNC_PIECE_COLW");
+        const int w = e ? atoi(e) : 0;
+        return (w == 1 || w == 2 || w == 4 || w == 8 || w == 16) ? w : 0;
+    }();
+    (void)n_in;
+    (void)blocks;
+    return forced;
+}
+
 // out rows r < n_out: dst[r·dst_row + 0 : width) = XOR_j coef[r·coef_row + j] · in[j·in_row + 0 : width), j < n_in.
 // coef: host memory; one row of at most kPieceInline bytes travels in the kernel arguments, more are read by the kernel
 // from ws->pc_coef (coef may already point there).  Synchronous: returns once dst holds every row.
@@ -264,8 +283,14 @@ int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t
     p.width = int64_t(width);
     p.n_in = int(n_in);
     p.n_out = int(n_out);
+    const int64_t gx = (p.width + rlnc::kPieceCols - 1) / rlnc::kPieceCols;
+    p.split = piece_split_for(p.n_in, gx * int64_t(n_out));
+    const int colw = p.split == 1 ? piece_col_waves_for(p.n_in, gx) : 0;
+    p.col_waves = colw ? 1 : 0;
+    const int waves = colw ? colw : piece_waves_for((p.n_in + p.split - 1) / p.split);
     p.chunk_blocks = piece_chunk_blocks();  // 64 KiB of a row per flag: the host copies one while the device writes on
-    const size_t chunks = size_t(rlnc::piece_chunks(p));
+    if (colw && !piece_chunk_forced()) p.chunk_blocks = std::max(1, p.chunk_blocks / colw);
+    const size_t chunks = size_t(rlnc::piece_chunks(p, waves));
     if (int st = ws->pc_out.ensure(n_out * size_t(p.out_row))) return st;
     if (chunks * 4 > ws->pc_flag.cap) {
         // completion is "flag == epoch" and every workspace counts its epochs from 1: a freshly allocated pinned
@@ -278,8 +303,6 @@ int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t
         HIP_TRY(hipMemsetAsync(ws->pc_count.p, 0, chunks * 4, ws->stream));
         ws->pc_count_words = chunks;
     }
-    const int64_t gx = (p.width + rlnc::kPieceCols - 1) / rlnc::kPieceCols;
-    p.split = piece_split_for(p.n_in, gx * int64_t(n_out));
     if (p.split > 1) {
         const size_t blocks = size_t(gx) * n_out;
         if (int st = ws->pc_part.ensure(blocks * size_t(p.split) * 64 * 16)) return st;
@@ -297,10 +320,10 @@ int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t
     if (++ws->epoch == 0) ws->epoch = 1;
     p.epoch = ws->epoch;
     const uint64_t t1 = g_piece_trace.on ? now_ns() : 0;
-    HIP_TRY(rlnc::launch_piece(p, piece_waves_for((p.n_in + p.split - 1) / p.split), ws->stream));
+    HIP_TRY(rlnc::launch_piece(p, waves, ws->stream));
     const uint64_t t2 = g_piece_trace.on ? now_ns() : 0;
     uint64_t t3 = 0;
-    const size_t chunk_bytes = size_t(p.chunk_blocks) * rlnc::kPieceCols;
+    const size_t chunk_bytes = size_t(p.chunk_blocks) * size_t(rlnc::piece_cols_per_wg(p, waves));
     const size_t cpr = chunks / n_out;
     for (size_t c = 0; c < chunks; ++c) {
         if (int st = piece_wait(p.flag + c, p.epoch, ws->stream)) {

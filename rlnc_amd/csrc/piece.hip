@@ -49,7 +49,7 @@ __device__ __forceinline__ void mac16(uint32_t (&acc)[4], const uint4 x, uint32_
     }
 }
 
-// grid (ceil(width / kPieceCols), n_out, split); block 64·W threads (W = 1, 2, 4, 8 or 16 waves)
+// grid (ceil(width / columns per workgroup), n_out, split); block 64·W threads (W = 1, 2, 4, 8 or 16 waves)
 __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PieceParams p) {
     __shared__ uint4 red[kPieceMaxWaves - 1][64];
     const int W = int(blockDim.x) >> 6;
@@ -58,9 +58,10 @@ __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PiecePara
     // this workgroup's sources: part z of `split` (z = blockIdx.z), then wave w's share of them
     const int RS = (p.n_in + p.split - 1) / p.split;
     const int s0 = min(p.n_in, int(blockIdx.z) * RS), s1 = min(p.n_in, s0 + RS);
-    const int R = (s1 - s0 + W - 1) / W;
-    const int r0 = min(s1, s0 + w * R), r1 = min(s1, r0 + R);
-    const int64_t col = int64_t(blockIdx.x) * kPieceCols + lane * 16;
+    const int R = p.col_waves ? s1 - s0 : (s1 - s0 + W - 1) / W;
+    const int r0 = p.col_waves ? s0 : min(s1, s0 + w * R), r1 = min(s1, r0 + R);
+    const int64_t cblk = p.col_waves ? int64_t(blockIdx.x) * W + w : int64_t(blockIdx.x);
+    const int64_t col = cblk * kPieceCols + lane * 16;
     const bool live = col < p.width;
     // source rows are padded to 16 bytes (in_row >= round16(width)): the last slot loads whole.  Every load is
     // unconditional from a valid address (lanes past the width read column 0, rows past the batch its last row), so
@@ -88,7 +89,7 @@ __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PiecePara
             }
         }
     }
-    if (W > 1) {
+    if (W > 1 && !p.col_waves) {
         if (w > 0) red[w - 1][lane] = make_uint4(acc[0], acc[1], acc[2], acc[3]);
         __syncthreads();
         if (w == 0)
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PiecePara
     // the workgroup is counted: every storing wave drains its stores, the workgroup meets at a barrier, one lane adds
     // to the chunk's counter (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms), and the chunk's last
     // workgroup raises the host flag with a write-through store
-    if (w == 0 && live) {
+    if ((w == 0 || p.col_waves) && live) {
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(p.out + int64_t(row) * p.out_row, 0, 0x7FFFFFFF, 0x00020000);
         const u32x4 v = {acc[0], acc[1], acc[2], acc[3]};
@@ -177,18 +178,21 @@ int piece_split(int n_in, int64_t blocks) {
     return std::min(32, (n_in + 63) / 64);
 }
 
-int piece_chunks(const PieceParams &p) {
-    const int64_t gx = (p.width + kPieceCols - 1) / kPieceCols;
+int piece_chunks(const PieceParams &p, int waves) {
+    const int64_t cw = piece_cols_per_wg(p, waves);
+    const int64_t gx = (p.width + cw - 1) / cw;
     return int((gx + p.chunk_blocks - 1) / p.chunk_blocks) * p.n_out;
 }
 
 hipError_t launch_piece(const PieceParams &p, int waves, hipStream_t s) {
-    const int64_t gx = (p.width + kPieceCols - 1) / kPieceCols;
+    const int64_t cw = piece_cols_per_wg(p, waves);
+    const int64_t gx = (p.width + cw - 1) / cw;
     if (p.n_in <= 0 || p.n_out <= 0 || p.n_out > 65535 || gx <= 0 || gx > 0x7FFFFFFFLL || p.chunk_blocks <= 0)
         return hipErrorInvalidValue;
     if (p.coef == nullptr && (p.n_out != 1 || p.n_in > kPieceInline)) return hipErrorInvalidValue;
     if (waves != 1 && waves != 2 && waves != 4 && waves != 8 && waves != 16) return hipErrorInvalidValue;
     if (p.split < 1 || p.split > 64 || (p.split > 1 && (p.part == nullptr || p.pcount == nullptr))) return hipErrorInvalidValue;
+    if (p.col_waves && p.split != 1) return hipErrorInvalidValue;
     if ((reinterpret_cast<uintptr_t>(p.in) | reinterpret_cast<uintptr_t>(p.out) | uintptr_t(p.in_row) |
          uintptr_t(p.out_row)) & 15)
         return hipErrorInvalidValue;

@@ -41,11 +41,18 @@ struct PieceParams {
     // coef == nullptr: the coefficients are these bytes (n_out == 1): read from the kernel-argument segment in device
     // memory instead of across PCIe from pinned host memory (a round trip at the head of every workgroup)
     uint8_t coef_inline[kPieceInline];
+    // col_waves != 0 (split == 1 only): the waves of a workgroup split the columns instead of the sources -- wave w
+    // owns column block blockIdx.x · W + w and walks every source, no LDS reduction -- so a workgroup covers
+    // W · kPieceCols columns and a narrow call launches W times fewer workgroups (chunk_blocks still counts workgroups)
+    int col_waves;
 };
+
+// columns one workgroup covers for `waves` waves per workgroup
+inline int64_t piece_cols_per_wg(const PieceParams &p, int waves) { return int64_t(kPieceCols) * (p.col_waves ? waves : 1); }
 
 int piece_waves(int n_in);  // waves per workgroup for n_in sources
 int piece_split(int n_in, int64_t blocks);  // workgroups per (row, column block) for n_in sources over `blocks` of them
-int piece_chunks(const PieceParams &p);
+int piece_chunks(const PieceParams &p, int waves);
 hipError_t launch_piece(const PieceParams &p, int waves, hipStream_t s);
 
 }  // namespace rlnc
