@@ -72,3 +72,16 @@ def test_two_ranks_config5_strong_split():
     assert line["config"]["objects_total"] == job  # the split covers every object of the fixed job exactly once
     assert line["config"]["objects_per_gpu"] == job // 2 + 1  # rank 0's share
     assert line["config"]["objects_per_launch"] == 8
+
+
+@pytest.mark.timeout(400)
+def test_four_ranks_config5_strong_split():
+    """Four ranks on the lease's GPU (profiles/r06_config5_n4_onegpu.json is the full job the same way): the ragged
+    split (35 = 9 + 9 + 9 + 8) covers the job once and every rank verifies its share."""
+    job = 35
+    line = run_bench(["--gpus", "4", "--workload", "config5", "--objects", str(job), "--chunk", "8", "--steps", "2",
+                      "--warmup", "1", "--breakdown-steps", "2", "--no-cpu-baseline", "--no-ceiling"])
+    check_common(line, n=4)
+    assert line["scaling"] == "strong"
+    assert line["config"]["objects_total"] == job
+    assert line["config"]["objects_per_gpu"] == job // 4 + 1  # rank 0's share
