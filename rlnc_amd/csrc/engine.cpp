@@ -238,14 +238,12 @@ bool piece_chunk_forced() {
 // Waves of a column-split workgroup (piece.hpp col_waves: each wave owns 1 KiB of columns and walks every source), or
 // 0 for the source-split form.  RLNC_PIECE_COLW (A/B knob, read once): W = column-split with W waves for every call
 // that does not split its sources over workgroups, 0 / unset = the source-split form
-int piece_col_waves_for(int n_in, int64_t blocks) {
+int piece_col_waves() {
     static const int forced = [] {
         const char *e = getenv("RLNC_PIECE_COLW");
         const int w = e ? atoi(e) : 0;
         return (w == 1 || w == 2 || w == 4 || w == 8 || w == 16) ? w : 0;
     }();
-    (void)n_in;
-    (void)blocks;
     return forced;
 }
 
@@ -285,7 +283,7 @@ int piece_call(CallWs *ws, const uint8_t *in, size_t in_row, size_t n_in, size_t
     p.n_out = int(n_out);
     const int64_t gx = (p.width + rlnc::kPieceCols - 1) / rlnc::kPieceCols;
     p.split = piece_split_for(p.n_in, gx * int64_t(n_out));
-    const int colw = p.split == 1 ? piece_col_waves_for(p.n_in, gx) : 0;
+    const int colw = p.split == 1 ? piece_col_waves() : 0;  // measured slower: off unless forced
     p.col_waves = colw ? 1 : 0;
     const int waves = colw ? colw : piece_waves_for((p.n_in + p.split - 1) / p.split);
     p.chunk_blocks = piece_chunk_blocks();  // 64 KiB of a row per flag: the host copies one while the device writes on
