@@ -222,6 +222,14 @@ bool piece_inline() {
     return on;
 }
 
+bool obj_warm() {
+    static const bool on = [] {
+        const char *e = getenv("RLNC_OBJ_WARM");
+        return e && atoi(e) != 0;
+    }();
+    return on;
+}
+
 int piece_chunk_blocks() {
     static const int c = [] {
         const char *e = getenv("RLNC_PIECE_CHUNK");  // A/B knob, read once: workgroups per completion flag
@@ -747,6 +755,12 @@ int rlnc_recoder_new(rlnc_context *ctx, const uint8_t *data, size_t len, size_t 
     if ((st = ws.acquire())) return st;
     HIP_TRY(hipMemcpy2DAsync(r->pieces, r->stride, data, full, full, n, hipMemcpyHostToDevice, ws->stream));
     HIP_TRY(hipStreamSynchronize(ws->stream));
+    if (obj_warm() && full <= kPieceMaxBytes && piece_eligible(r->pieces, r->stride, full)) {
+        // A/B knob RLNC_OBJ_WARM=1: one throwaway call-kernel pass over the fresh pieces (zero coefficients, the recode
+        // call's grid, so each workgroup's lines land in the L2 of the XCD that will read them)
+        std::vector<uint8_t> zc(n, 0), scratch(full);
+        if ((st = piece_call(ws.ws.get(), r->pieces, r->stride, n, full, zc.data(), n, 1, scratch.data(), full))) return st;
+    }
     *out = r.release();
     return RLNC_OK;
 }
