@@ -222,6 +222,16 @@ bool piece_inline() {
     return on;
 }
 
+constexpr size_t kGridUploadMax = size_t(8) << 20;  // Recoder::new uploads up to this many bytes by the grid kernel
+
+bool grid_upload() {
+    static const bool on = [] {
+        const char *e = getenv("RLNC_GRID_UPLOAD");  // A/B knob, read once: 0 = the DMA upload for every object
+        return !e || atoi(e) != 0;
+    }();
+    return on;
+}
+
 bool obj_warm() {
     static const bool on = [] {
         const char *e = getenv("RLNC_OBJ_WARM");
@@ -753,7 +763,17 @@ int rlnc_recoder_new(rlnc_context *ctx, const uint8_t *data, size_t len, size_t 
     if ((st = ctx->obj_alloc(n * r->stride, &r->pieces, &r->pieces_cap))) return st;
     Lease ws(ctx);
     if ((st = ws.acquire())) return st;
-    HIP_TRY(hipMemcpy2DAsync(r->pieces, r->stride, data, full, full, n, hipMemcpyHostToDevice, ws->stream));
+    if (full % 16 == 0 && full <= kPieceMaxBytes && n * full <= kGridUploadMax && grid_upload() &&
+        piece_eligible(r->pieces, r->stride, full)) {
+        // small objects: staged through the lease's pinned buffer and copied by a kernel on the recode call's grid, so
+        // the recode calls that follow find the pieces in the reading XCDs' L2 (piece.hip piece_upload_kernel)
+        if ((st = ws->pc_coef.ensure(n * full))) return st;
+        std::memcpy(ws->pc_coef.p, data, n * full);
+        HIP_TRY(rlnc::launch_piece_upload(ws->pc_coef.as<uint8_t>(), int64_t(full), r->pieces, int64_t(r->stride),
+                                          int64_t(full), int(n), ws->stream));
+    } else {
+        HIP_TRY(hipMemcpy2DAsync(r->pieces, r->stride, data, full, full, n, hipMemcpyHostToDevice, ws->stream));
+    }
     HIP_TRY(hipStreamSynchronize(ws->stream));
     if (obj_warm() && full <= kPieceMaxBytes && piece_eligible(r->pieces, r->stride, full)) {
         // A/B knob RLNC_OBJ_WARM=1: one throwaway call-kernel pass over the fresh pieces (zero coefficients, the recode

@@ -160,7 +160,33 @@ __global__ __launch_bounds__(64 * kPieceMaxWaves) void gf_piece_kernel(PiecePara
     }
 }
 
+// Recoder::new's upload of small objects: dst row j = src row j (src: pinned host memory), on the call kernel's grid
+// (x = 1 KiB column block, one workgroup per block) so that each block's lines are written through the L2 of the XCD
+// the recode call's workgroup for that block runs on, and its loads hit there instead of HBM (the DMA upload leaves
+// them cold: 1.2-1.8 us per call, profiles/r06_objwarm_ab.txt).  width, src_row, dst_row multiples of 16.
+__global__ __launch_bounds__(256) void piece_upload_kernel(const uint8_t *src, int64_t src_row, uint8_t *dst,
+                                                          int64_t dst_row, int64_t width, int n) {
+    const int W = int(blockDim.x) >> 6;
+    const int w = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
+    const int64_t col = int64_t(blockIdx.x) * kPieceCols + lane * 16;
+    if (col >= width) return;
+    for (int j = w; j < n; j += W)
+        *reinterpret_cast<uint4 *>(dst + int64_t(j) * dst_row + col) =
+            *reinterpret_cast<const uint4 *>(src + int64_t(j) * src_row + col);
+}
+
 }  // namespace
+
+hipError_t launch_piece_upload(const uint8_t *src, int64_t src_row, uint8_t *dst, int64_t dst_row, int64_t width, int n,
+                               hipStream_t s) {
+    if (n <= 0 || width <= 0 || ((width | src_row | dst_row) & 15) || src_row < width || dst_row < width ||
+        ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15))
+        return hipErrorInvalidValue;
+    const int64_t gx = (width + kPieceCols - 1) / kPieceCols;
+    if (gx > 0x7FFFFFFFLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(piece_upload_kernel, dim3(unsigned(gx)), dim3(256), 0, s, src, src_row, dst, dst_row, width, n);
+    return hipGetLastError();
+}
 
 // rows per wave: 2-8 for up to 32 sources (4 waves), 8-16 for up to 128 (8 waves), 16 waves beyond -- the fastest of
 // 2/4/8/16 waves at each of the reference's 1 MB bench shapes (profiles/r04_piece_waves_ab.txt; one wave per source

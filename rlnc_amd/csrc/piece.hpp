@@ -54,5 +54,8 @@ int piece_waves(int n_in);  // waves per workgroup for n_in sources
 int piece_split(int n_in, int64_t blocks);  // workgroups per (row, column block) for n_in sources over `blocks` of them
 int piece_chunks(const PieceParams &p, int waves);
 hipError_t launch_piece(const PieceParams &p, int waves, hipStream_t s);
+// dst row j = src row j (j < n) over width bytes on the call kernel's column-block grid (src may be pinned host memory)
+hipError_t launch_piece_upload(const uint8_t *src, int64_t src_row, uint8_t *dst, int64_t dst_row, int64_t width, int n,
+                               hipStream_t s);
 
 }  // namespace rlnc
